@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident coprocessor NF pipeline, Mpkt/s (BASELINE.json).
+
+A step = one pass of the pipeline over one batch of synthetic packets that
+are already resident in HBM. Default workload = BASELINE configs[1]:
+firewall ACL (1k rules), 64 B packets, batch 64k. The timed region rotates
+over a pool of distinct batches larger than the 256 MiB Infinity Cache, so
+every step reads its packets from HBM.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one
+process per GPU, each with its own context, batches and tables (the path
+shards with no data-path collective: weak scaling). A gloo barrier
+brackets the timed region and the max elapsed time over ranks is used.
+
+Also reported (rank 0):
+  roofline      algorithmic bytes per launch / mean kernel time (HIP events
+                on the context's stream around every launch), vs 8 TB/s;
+  cpu_baseline  the oracle's restatement of the reference CPU coprocessor()
+                loop (oracle/cop_oracle.c), 1 pinned core, bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ghost-dataplane_amd"))
+
+import copgpu as cg  # noqa: E402
+
+METRIC = "Mpkt/s device-resident coprocessor NF pipeline (64B pkts); HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
+# config_id follows BASELINE.json configs[] (1-based); seeds per SURVEY.md §8d
+WORKLOADS = {
+    "fw1k": dict(cid=2, stages=S | F, fw=1000, routes=0, imix=False, batch=65536,
+                 desc="firewall ACL 1k rules, 64B pkts, batch 64k (BASELINE configs[1])"),
+    "fw_lpm_imix": dict(cid=3, stages=S | F | L, fw=1000, routes=100000, imix=True, batch=65536,
+                        desc="firewall + LPM 100k prefixes, IMIX, batch 64k (BASELINE configs[2])"),
+    "fw_lpm": dict(cid=4, stages=S | F | L, fw=1000, routes=100000, imix=False, batch=65536,
+                   desc="firewall + LPM 100k, 64B pkts, batch 64k per GPU (BASELINE configs[3])"),
+    "fw_lpm_1m": dict(cid=5, stages=S | F | L, fw=1000000, routes=1000000, imix=False, batch=262144,
+                      desc="1M ACL rules + 1M LPM prefixes, 64B, batch 256k per GPU (BASELINE configs[4])"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=480)
+    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--workload", default="fw1k", choices=sorted(WORKLOADS))
+    ap.add_argument("--per-launch", type=int, default=16, help="batches per kernel launch")
+    ap.add_argument("--pool-mib", type=int, default=400, help="distinct input bytes per GPU")
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    W = WORKLOADS[args.workload]
+    B = W["batch"]
+    Lb = max(1, min(args.per_launch, 32))
+
+    lib = cg.lib()   # load the HIP runtime the product links (before torch)
+    ndev = cg.device_count()
+    if ndev < 1:
+        raise SystemExit("bench: no GPU visible")
+    dev = local % ndev
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo", rank=rank, world_size=world)
+        dist = (torch, tdist)
+
+    # ---- tables (identical on every rank; packets differ per rank) ----
+    cid = W["cid"]
+    t0 = time.time()
+    fw_rules = cg.gen_rules(0x5EED1000 + cid, W["fw"], cg.GEN_FW, 20 if W["fw"] <= 1000 else 0)
+    routes = cg.gen_rules(0x5EED2000 + cid, W["routes"], cg.GEN_ROUTES, 0) if W["routes"] else None
+    if W["fw"] <= 1024:
+        fw_tab = cg.LpmTable(fw_rules, 1024, 24, True)                  # lpm_setup's own limits
+    else:
+        fw_tab = cg.LpmTable(fw_rules, W["fw"], 1 << 20, False)
+    ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32)
+    ctx.set_fw_table(fw_tab)
+    if routes is not None:
+        ctx.set_route_lpm(cg.LpmTable(routes, max(W["routes"], 1), 1 << 20, False))
+    log(f"[rank {rank}] tables ready in {time.time() - t0:.1f}s on device {dev}")
+
+    # ---- input pool: distinct batches, > Infinity Cache ----
+    pool_bytes = args.pool_mib << 20
+    t0 = time.time()
+    if W["imix"]:
+        slab, offs = cg.gen_imix(0x5EED0000 + cid + 1000 * rank, B, fw_rules, routes)
+        per_batch = slab.nbytes + offs.nbytes
+    else:
+        per_batch = B * 64
+    P = max(2, pool_bytes // per_batch)
+    d_pkts = ctx.alloc(P * per_batch)
+    d_res = ctx.alloc(P * B * 8)
+    d_fwd = ctx.alloc(P * B * 4)
+    d_cnt = ctx.alloc(P * 4 + 16)
+    if W["imix"]:
+        # same packet mix in every batch slot, distinct addresses
+        for i in range(P):
+            d_pkts.upload(slab, i * per_batch)
+            d_pkts.upload(offs, i * per_batch + slab.nbytes)
+    else:
+        chunk = 16
+        for i in range(0, P, chunk):
+            k = min(chunk, P - i)
+            pk = cg.gen_trace(0x5EED0000 + cid + 1000 * rank + i, k * B, fw_rules, routes)
+            d_pkts.upload(pk, i * per_batch)
+    log(f"[rank {rank}] pool: {P} batches x {B} pkts ({P * per_batch / 2**20:.0f} MiB) in {time.time() - t0:.1f}s")
+
+    def batch(i):
+        i %= P
+        if W["imix"]:
+            base = d_pkts.addr + i * per_batch
+            return cg.make_batch(base, B, d_res.addr + i * B * 8, offsets=base + slab.nbytes,
+                                 fwd_idx=d_fwd.addr + i * B * 4, fwd_count=d_cnt.addr + i * 4)
+        return cg.make_batch(d_pkts.addr + i * per_batch, B, d_res.addr + i * B * 8, stride=64,
+                             fwd_idx=d_fwd.addr + i * B * 4, fwd_count=d_cnt.addr + i * 4)
+
+    def run_steps(first, count):
+        s = first
+        while s < first + count:
+            k = min(Lb, first + count - s)
+            ctx.submit([batch(s + j) for j in range(k)])
+            s += k
+
+    def barrier():
+        if dist:
+            dist[1].barrier()
+
+    # ---- warmup, then exactly K timed steps ----
+    run_steps(0, args.warmup)
+    ctx.sync()
+    barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    run_steps(args.warmup, args.steps)
+    ctx.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist:
+        torch, tdist = dist
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_pkts = world * args.steps * B
+    value = total_pkts / elapsed / 1e6
+    log(f"[rank {rank}] timed {args.steps} steps in {elapsed * 1e3:.2f} ms -> {value:.1f} Mpkt/s (all ranks)")
+
+    # ---- kernel duration per launch (HIP events on the context stream) ----
+    ctx.launch_timing(True)
+    nl = max(8, args.steps // Lb)
+    run_steps(0, nl * Lb)
+    ctx.sync()
+    mean_ms, n_launch = ctx.launch_timing_read(reset=True)
+    ctx.launch_timing(False)
+    bytes_per_pkt = 76 if W["imix"] else 72   # 64 B header line (+4 B offset) + 8 B record
+    alg_bytes = bytes_per_pkt * B * Lb
+    achieved = alg_bytes / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
+
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_L{Lb}.json")
+    if os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "Mpkt/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (splitmix64 64B Eth/IPv4/UDP frames and rule sets, SURVEY.md §8d seeds)",
+        "config": {
+            "workload": args.workload,
+            "description": W["desc"],
+            "batch": B,
+            "batches_per_launch": Lb,
+            "fw_rules": W["fw"],
+            "route_prefixes": W["routes"],
+            "pkt_layout": "imix slab + u32 offsets" if W["imix"] else "64B slots",
+            "stages": W["stages"],
+            "parallelism": f"independent per-GPU contexts x{world} (no data-path collective)",
+            "pool_batches": int(P),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_pkt": bytes_per_pkt,
+            "kernel_ms_per_launch": round(mean_ms, 6),
+            "launches_timed": int(n_launch),
+        },
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as orc   # CPU baseline leg only
+        ofw = orc.OracleLpm(max(1024, W["fw"]), 24 if W["fw"] <= 1000 else 1 << 20)
+        ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=W["fw"] <= 1000)
+        ns = 131072
+        trace = cg.gen_trace(0x5EED0001, ns, fw_rules, None)   # configs[0] seed: CPU reference case
+        rate, pk, secs = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget, 1, 0)
+        out["cpu_baseline"] = {
+            "value": round(rate, 3),
+            "unit": "Mpkt/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": (f"{pk} packets through the restated coprocessor() loop (burst 32, 16384-slot "
+                       f"SPSC ring, 2176 B mbufs, DIR-24-8 firewall, {W['fw']} rules), "
+                       f"{secs:.1f} s on 1 pinned core"),
+        }
+        log(f"[rank 0] cpu baseline {rate:.1f} Mpkt/s on 1 core ({pk} pkts)")
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist[1].destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

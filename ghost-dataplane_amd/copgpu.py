@@ -1,0 +1,440 @@
+"""ctypes binding of libcopgpu.so (the C ABI in include/cop_gpu.h).
+
+This is the Python face of the drop-in boundary: tests and bench.py call
+the HIP pipeline only through these C entry points. There is no CPU
+fallback: if libcopgpu.so is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, byref, c_char_p, c_double, c_int, c_int32,
+                    c_size_t, c_uint8, c_uint16, c_uint32, c_uint64, c_void_p)
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcopgpu.so")
+
+# ---------------------------------------------------------------------------
+# constants (include/cop_gpu.h)
+STAGE_PARSE, STAGE_FW, STAGE_LPM = 0x1, 0x2, 0x4
+FORWARD, DROP_FW, DROP_PARSE, DROP_NOT_IPV4, DROP_NO_PORT = 0, 1, 2, 3, 4
+FLAG_ROUTE_HIT, FLAG_FW_HIT = 0x1, 0x2
+LPM_STOP_AT_FIRST_ERROR = 0x1
+CFG_FW_FORCE_DIR24, CFG_LPM_FORCE_DIR24, CFG_NO_COMPACT = 0x1, 0x2, 0x4
+GEN_FW, GEN_ROUTES = 0, 1
+UNKNOWN_PORT = 0xFFFF
+
+PREFIX_DT = np.dtype([("ip", "<u4"), ("next_hop", "<u4"), ("depth", "u1"), ("_pad", "u1", (3,))])
+RESULT_DT = np.dtype([("verdict", "u1"), ("flags", "u1"), ("port", "<u2"), ("route_nh", "<u4")])
+COUNTER_NAMES = ["pkt_drop", "pkt_accept", "pkt_not_ipv4", "pkt_total", "parse_err", "no_port",
+                 "forward", "route_hit", "rx"]
+
+
+class CopError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__(f"cop error {code}: {msg}")
+        self.code = code
+
+
+class LpmConfig(Structure):
+    _fields_ = [("max_rules", c_uint32), ("number_tbl8s", c_uint32), ("flags", c_uint32)]
+
+
+class LpmReport(Structure):
+    _fields_ = [("n_in", c_uint32), ("n_added", c_uint32), ("n_distinct", c_uint32),
+                ("n_updated", c_uint32), ("n_failed", c_uint32), ("n_skipped", c_uint32),
+                ("first_error", c_int32), ("first_error_idx", c_uint32), ("tbl8_used", c_uint32),
+                ("n_intervals", c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Config(Structure):
+    _fields_ = [("device", c_int), ("stages", c_uint32), ("n_ports", c_uint32),
+                ("max_batch", c_uint32), ("max_batches", c_uint32), ("flags", c_uint32),
+                ("routing_table", POINTER(c_uint16))]
+
+
+class Batch(Structure):
+    _fields_ = [("pkts", c_void_p), ("offsets", c_void_p), ("n", c_uint32), ("stride", c_uint32),
+                ("data_off", c_uint32), ("_pad", c_uint32), ("results", c_void_p),
+                ("fwd_idx", c_void_p), ("fwd_count", c_void_p)]
+
+
+class TraceOpts(Structure):
+    _fields_ = [("n_ports", c_uint32), ("pct_non_ipv4", c_uint32), ("pct_bad_version", c_uint32),
+                ("pct_unknown_dst", c_uint32), ("pct_vport_dst", c_uint32),
+                ("pct_src_in_rule", c_uint32)]
+
+
+class NfStats(Structure):
+    _fields_ = [("rx_packets", c_uint64), ("rx_dropped", c_uint64), ("tx_packets", c_uint64),
+                ("tx_dropped", c_uint64)]
+
+
+# every function declared in include/cop_gpu.h: name -> (restype, argtypes)
+SIGNATURES = {
+    "cop_lpm_build": (c_int, [c_void_p, c_uint32, POINTER(LpmConfig), POINTER(c_void_p), POINTER(LpmReport)]),
+    "cop_lpm_free": (None, [c_void_p]),
+    "cop_lpm_export_dir24": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32]),
+    "cop_lpm_export_intervals": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32]),
+    "cop_lpm_export_rules": (c_int, [c_void_p, c_void_p, c_uint32]),
+    "cop_rules_load_json": (c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
+    "cop_rules_free": (None, [c_void_p]),
+    "cop_rules_write_json": (c_int, [c_char_p, c_void_p, c_uint32]),
+    "cop_route_table_default": (None, [c_void_p, c_uint32]),
+    "cop_config_default": (None, [POINTER(Config)]),
+    "cop_create": (c_int, [POINTER(Config), POINTER(c_void_p)]),
+    "cop_destroy": (None, [c_void_p]),
+    "cop_last_error": (c_char_p, [c_void_p]),
+    "cop_device_count": (c_int, []),
+    "cop_set_fw_table": (c_int, [c_void_p, c_void_p]),
+    "cop_set_route_lpm": (c_int, [c_void_p, c_void_p]),
+    "cop_set_routing_table": (c_int, [c_void_p, c_void_p]),
+    "cop_load_fw_rules_file": (c_int, [c_void_p, c_char_p, POINTER(LpmConfig), POINTER(LpmReport)]),
+    "cop_submit": (c_int, [c_void_p, POINTER(Batch), c_uint32]),
+    "cop_sync": (c_int, [c_void_p]),
+    "cop_poll": (c_int, [c_void_p]),
+    "cop_process_host": (c_int, [c_void_p, POINTER(c_void_p), c_uint32, c_void_p, c_void_p, c_void_p]),
+    "cop_counters_read": (c_int, [c_void_p, c_void_p, c_int]),
+    "cop_counters_device_ptr": (c_void_p, [c_void_p]),
+    "cop_dev_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    "cop_dev_free": (c_int, [c_void_p, c_void_p]),
+    "cop_host_alloc_pinned": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    "cop_host_free_pinned": (c_int, [c_void_p, c_void_p]),
+    "cop_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "cop_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "cop_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "cop_memset_d": (c_int, [c_void_p, c_void_p, c_int, c_size_t]),
+    "cop_timer_start": (c_int, [c_void_p]),
+    "cop_timer_stop": (c_int, [c_void_p, POINTER(c_double)]),
+    "cop_launch_timing": (c_int, [c_void_p, c_int]),
+    "cop_launch_timing_read": (c_int, [c_void_p, POINTER(c_double), POINTER(c_uint64), c_int]),
+    "cop_ring_create": (c_void_p, [c_uint32]),
+    "cop_ring_free": (None, [c_void_p]),
+    "cop_ring_enqueue_bulk": (c_uint32, [c_void_p, c_void_p, c_uint32, POINTER(c_uint32)]),
+    "cop_ring_dequeue_burst": (c_uint32, [c_void_p, c_void_p, c_uint32, POINTER(c_uint32)]),
+    "cop_ring_count": (c_uint32, [c_void_p]),
+    "cop_set_mbuf_layout": (None, [c_uint32, c_uint32]),
+    "cop_set_rule_file": (None, [c_char_p]),
+    "coprocessor_setup": (c_int, []),
+    "coprocessor_teardown": (c_int, []),
+    "process_packet": (c_int, [c_void_p]),
+    "process_burst": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "cop_coprocessor_poll": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, POINTER(NfStats)]),
+    "coprocessor_ctx": (c_void_p, []),
+    "cop_gen_rules": (c_int, [c_uint64, c_uint32, c_int, c_uint32, c_void_p]),
+    "cop_trace_opts_default": (None, [POINTER(TraceOpts)]),
+    "cop_gen_trace": (c_int, [c_uint64, c_uint32, POINTER(TraceOpts), c_void_p, c_uint32, c_void_p,
+                              c_uint32, c_void_p, c_uint32]),
+    "cop_gen_imix": (c_int, [c_uint64, c_uint32, POINTER(TraceOpts), c_void_p, c_uint32, c_void_p,
+                             c_uint32, c_void_p, POINTER(c_uint64), c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libcopgpu.so (raises ImportError when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built (run make -C ghost-dataplane_amd)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(c_void_p) if a is not None else None
+
+
+def _check(rc, ctx=None, what=""):
+    if rc < 0:
+        msg = what
+        if ctx is not None and ctx.handle:
+            msg += ": " + lib().cop_last_error(ctx.handle).decode(errors="replace")
+        raise CopError(rc, msg)
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# host helpers
+
+def prefixes(ip, depth, next_hop) -> np.ndarray:
+    ip = np.asarray(ip, dtype=np.uint64)
+    a = np.zeros(len(ip), dtype=PREFIX_DT)
+    a["ip"] = ip.astype(np.uint32)
+    a["depth"] = np.asarray(depth, dtype=np.int64).astype(np.uint8)
+    a["next_hop"] = np.asarray(next_hop, dtype=np.uint64).astype(np.uint32)
+    return a
+
+
+def gen_rules(seed: int, n: int, kind: int = GEN_FW, n_long_parents: int = 20) -> np.ndarray:
+    out = np.zeros(n, dtype=PREFIX_DT)
+    _check(lib().cop_gen_rules(seed, n, kind, n_long_parents, _ptr(out)), what="gen_rules")
+    return out
+
+
+def trace_opts(**kw) -> TraceOpts:
+    o = TraceOpts()
+    lib().cop_trace_opts_default(byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def gen_trace(seed: int, n: int, fw=None, routes=None, stride: int = 64, opts: TraceOpts | None = None,
+              out: np.ndarray | None = None) -> np.ndarray:
+    if out is None:
+        out = np.zeros(n * stride, dtype=np.uint8)
+    fw = fw if fw is not None else np.zeros(0, dtype=PREFIX_DT)
+    routes = routes if routes is not None else np.zeros(0, dtype=PREFIX_DT)
+    _check(lib().cop_gen_trace(seed, n, byref(opts) if opts else None, _ptr(fw), len(fw), _ptr(routes),
+                               len(routes), _ptr(out), stride), what="gen_trace")
+    return out
+
+
+def gen_imix(seed: int, n: int, fw=None, routes=None, opts: TraceOpts | None = None):
+    fw = fw if fw is not None else np.zeros(0, dtype=PREFIX_DT)
+    routes = routes if routes is not None else np.zeros(0, dtype=PREFIX_DT)
+    size = c_uint64(0)
+    o = byref(opts) if opts else None
+    _check(lib().cop_gen_imix(seed, n, o, _ptr(fw), len(fw), _ptr(routes), len(routes), None, byref(size), None))
+    slab = np.zeros(size.value + 64, dtype=np.uint8)
+    offs = np.zeros(n, dtype=np.uint32)
+    _check(lib().cop_gen_imix(seed, n, o, _ptr(fw), len(fw), _ptr(routes), len(routes), _ptr(slab),
+                              byref(size), _ptr(offs)))
+    return slab, offs
+
+
+def route_table_default(n_ports: int = 5) -> np.ndarray:
+    rt = np.zeros(65536, dtype=np.uint16)
+    lib().cop_route_table_default(_ptr(rt), n_ports)
+    return rt
+
+
+def rules_load_json(path: str) -> np.ndarray:
+    p = c_void_p()
+    n = c_uint32()
+    _check(lib().cop_rules_load_json(path.encode(), byref(p), byref(n)), what=f"load {path}")
+    try:
+        buf = (ctypes.c_uint8 * (n.value * PREFIX_DT.itemsize)).from_address(p.value) if n.value else b""
+        return np.frombuffer(bytes(buf), dtype=PREFIX_DT).copy()
+    finally:
+        lib().cop_rules_free(p)
+
+
+def rules_write_json(path: str, rules: np.ndarray):
+    rules = np.ascontiguousarray(rules, dtype=PREFIX_DT)
+    _check(lib().cop_rules_write_json(path.encode(), _ptr(rules), len(rules)), what=f"write {path}")
+
+
+class LpmTable:
+    """Host-built LPM table with DPDK rte_lpm_add semantics."""
+
+    def __init__(self, rules: np.ndarray, max_rules=1024, number_tbl8s=24, stop_at_first_error=True):
+        rules = np.ascontiguousarray(rules, dtype=PREFIX_DT)
+        cfg = LpmConfig(max_rules, number_tbl8s, LPM_STOP_AT_FIRST_ERROR if stop_at_first_error else 0)
+        self.handle = c_void_p()
+        self.report = LpmReport()
+        _check(lib().cop_lpm_build(_ptr(rules), len(rules), byref(cfg), byref(self.handle),
+                                   byref(self.report)), what="cop_lpm_build")
+
+    def __del__(self):
+        if getattr(self, "handle", None) and self.handle.value:
+            lib().cop_lpm_free(self.handle)
+            self.handle = c_void_p()
+
+    def rules(self) -> np.ndarray:
+        n = _check(lib().cop_lpm_export_rules(self.handle, None, 0))
+        out = np.zeros(n, dtype=PREFIX_DT)
+        _check(lib().cop_lpm_export_rules(self.handle, _ptr(out), n))
+        return out
+
+    def intervals(self):
+        m = _check(lib().cop_lpm_export_intervals(self.handle, None, None, 1 << 31))
+        s = np.zeros(m, dtype=np.uint32)
+        v = np.zeros(m, dtype=np.uint32)
+        _check(lib().cop_lpm_export_intervals(self.handle, _ptr(s), _ptr(v), m))
+        return s, v
+
+    def dir24(self):
+        t24 = np.zeros(1 << 24, dtype=np.uint32)
+        cap = 256 * max(1, self.report.n_distinct)
+        t8 = np.zeros(cap, dtype=np.uint32)
+        n_ext = _check(lib().cop_lpm_export_dir24(self.handle, _ptr(t24), _ptr(t8), cap))
+        return t24, t8[: n_ext * 256]
+
+
+class DeviceBuffer:
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        self.ptr = c_void_p()
+        _check(lib().cop_dev_alloc(ctx.handle, self.nbytes, byref(self.ptr)), ctx, "dev_alloc")
+
+    @property
+    def addr(self) -> int:
+        return self.ptr.value
+
+    def upload(self, a: np.ndarray, offset: int = 0):
+        a = np.ascontiguousarray(a)
+        assert offset + a.nbytes <= self.nbytes
+        _check(lib().cop_memcpy_h2d(self.ctx.handle, c_void_p(self.addr + offset), _ptr(a), a.nbytes),
+               self.ctx, "h2d")
+
+    def download(self, dtype, count: int, offset: int = 0) -> np.ndarray:
+        out = np.zeros(count, dtype=dtype)
+        assert offset + out.nbytes <= self.nbytes
+        if out.nbytes:
+            _check(lib().cop_memcpy_d2h(self.ctx.handle, _ptr(out), c_void_p(self.addr + offset), out.nbytes),
+                   self.ctx, "d2h")
+        return out
+
+    def fill(self, value: int = 0):
+        _check(lib().cop_memset_d(self.ctx.handle, self.ptr, value, self.nbytes), self.ctx, "memset")
+
+    def free(self):
+        if self.ptr.value:
+            lib().cop_dev_free(self.ctx.handle, self.ptr)
+            self.ptr = c_void_p()
+
+    def __del__(self):
+        try:
+            if self.ptr.value and self.ctx.handle:
+                self.free()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    return lib().cop_device_count()
+
+
+class Context:
+    """One GPU context (cop_ctx): device, stream, NF tables."""
+
+    def __init__(self, device=0, stages=STAGE_PARSE | STAGE_FW, n_ports=5, max_batch=262144,
+                 max_batches=32, flags=0, routing_table: np.ndarray | None = None):
+        cfg = Config()
+        lib().cop_config_default(byref(cfg))
+        cfg.device, cfg.stages, cfg.n_ports = device, stages, n_ports
+        cfg.max_batch, cfg.max_batches, cfg.flags = max_batch, max_batches, flags
+        self._rt = None
+        if routing_table is not None:
+            self._rt = np.ascontiguousarray(routing_table, dtype=np.uint16)
+            cfg.routing_table = self._rt.ctypes.data_as(POINTER(c_uint16))
+        self.handle = c_void_p()
+        rc = lib().cop_create(byref(cfg), byref(self.handle))
+        if rc < 0:
+            raise CopError(rc, "cop_create failed (no GPU?)")
+        self.cfg = cfg
+
+    def close(self):
+        if self.handle and self.handle.value:
+            lib().cop_destroy(self.handle)
+            self.handle = c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_fw_table(self, t: LpmTable):
+        _check(lib().cop_set_fw_table(self.handle, t.handle), self, "set_fw_table")
+
+    def set_route_lpm(self, t: LpmTable):
+        _check(lib().cop_set_route_lpm(self.handle, t.handle), self, "set_route_lpm")
+
+    def set_routing_table(self, rt: np.ndarray):
+        rt = np.ascontiguousarray(rt, dtype=np.uint16)
+        assert rt.size == 65536
+        _check(lib().cop_set_routing_table(self.handle, _ptr(rt)), self, "set_routing_table")
+
+    def load_fw_rules_file(self, path, max_rules=1024, number_tbl8s=24, stop_at_first_error=True):
+        cfg = LpmConfig(max_rules, number_tbl8s, LPM_STOP_AT_FIRST_ERROR if stop_at_first_error else 0)
+        rep = LpmReport()
+        _check(lib().cop_load_fw_rules_file(self.handle, path.encode(), byref(cfg), byref(rep)), self,
+               "load_fw_rules_file")
+        return rep
+
+    def alloc(self, nbytes) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def submit(self, batches):
+        arr = (Batch * len(batches))(*batches)
+        _check(lib().cop_submit(self.handle, arr, len(batches)), self, "submit")
+
+    def sync(self):
+        _check(lib().cop_sync(self.handle), self, "sync")
+
+    def counters(self, reset=False) -> dict:
+        c = np.zeros(16, dtype=np.uint64)
+        _check(lib().cop_counters_read(self.handle, _ptr(c), 1 if reset else 0), self, "counters")
+        return {k: int(c[i]) for i, k in enumerate(COUNTER_NAMES)}
+
+    def counters_device_ptr(self) -> int:
+        return lib().cop_counters_device_ptr(self.handle)
+
+    def process_host(self, pkts: np.ndarray, n: int, stride: int = 64):
+        """End-to-end: host packet memory -> pinned gather -> H2D -> kernel -> D2H."""
+        base = pkts.ctypes.data
+        ptrs = (c_void_p * n)(*[base + i * stride for i in range(n)])
+        res = np.zeros(n, dtype=RESULT_DT)
+        fwd = np.zeros(max(n, 1), dtype=np.uint32)
+        cnt = c_uint32(0)
+        _check(lib().cop_process_host(self.handle, ptrs, n, _ptr(res), _ptr(fwd), byref(cnt)), self,
+               "process_host")
+        return res, fwd[: cnt.value]
+
+    def timer_start(self):
+        _check(lib().cop_timer_start(self.handle), self, "timer_start")
+
+    def timer_stop(self) -> float:
+        ms = c_double(0)
+        _check(lib().cop_timer_stop(self.handle, byref(ms)), self, "timer_stop")
+        return ms.value
+
+    def launch_timing(self, enable=True):
+        _check(lib().cop_launch_timing(self.handle, 1 if enable else 0), self, "launch_timing")
+
+    def launch_timing_read(self, reset=True):
+        ms = c_double(0)
+        n = c_uint64(0)
+        _check(lib().cop_launch_timing_read(self.handle, byref(ms), byref(n), 1 if reset else 0), self,
+               "launch_timing_read")
+        return ms.value, n.value
+
+
+def make_batch(pkts: DeviceBuffer | int, n: int, results: DeviceBuffer | int, stride: int = 64,
+               offsets: DeviceBuffer | int | None = None, fwd_idx=None, fwd_count=None,
+               data_off: int = 0, pkts_offset: int = 0, results_offset: int = 0) -> Batch:
+    def addr(x, off=0):
+        if x is None:
+            return None
+        return (x.addr if isinstance(x, DeviceBuffer) else int(x)) + off
+    b = Batch()
+    b.pkts = addr(pkts, pkts_offset)
+    b.offsets = addr(offsets)
+    b.n = n
+    b.stride = stride
+    b.data_off = data_off
+    b.results = addr(results, results_offset)
+    b.fwd_idx = addr(fwd_idx)
+    b.fwd_count = addr(fwd_count)
+    return b

@@ -1,0 +1,51 @@
+/*
+ * cop_internal.h — host-side structures shared between the C setup code
+ * (LPM builder, rules loader) and the HIP runtime. Not part of the ABI.
+ */
+#ifndef COP_INTERNAL_H
+#define COP_INTERNAL_H
+
+#include <stdint.h>
+#include "cop_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Internal interval value: bits 0-23 next hop, bit 24 hit, bits 26-31 depth
+ * of the matching rule (0 on a miss). Lookups only observe bits 0-24. */
+#define COP_IV_HIT      0x01000000u
+#define COP_IV_NHHIT    0x01FFFFFFu
+#define COP_IV_DEPTH_SH 26
+
+/* DIR-24-8 entry bits (DPDK v1604 rte_lpm_tbl_entry, little-endian). */
+#define COP_DIR_VALID     0x01000000u
+#define COP_DIR_EXT       0x02000000u
+#define COP_DIR_VALID_EXT 0x03000000u
+
+struct cop_lpm_table {
+    /* accepted rule set (masked prefix, depth, final next hop) */
+    uint32_t  n_rules;
+    uint32_t *rule_ip;
+    uint8_t  *rule_depth;
+    uint32_t *rule_nh;
+    /* flattened function over [0, 2^32): starts ascending, starts[0] = 0 */
+    uint32_t  n_iv;
+    uint32_t *iv_start;
+    uint32_t *iv_val;      /* internal value incl. depth */
+    uint32_t  tbl8_used;   /* DPDK-semantics tbl8 groups (acceptance) */
+    uint32_t  n_ext;       /* /24 blocks that need a tbl8 group in our image */
+    cop_lpm_report report;
+};
+
+/* Flatten (hit,nh) only: merged interval arrays for the LDS search form.
+ * Returns the count; the starts and vals arrays are malloc-ed. */
+uint32_t cop_lpm_merged_intervals(const cop_lpm_table *t, uint32_t **starts, uint32_t **vals);
+/* Build the DIR-24-8 image into caller buffers (tbl24: 1<<24 entries,
+ * tbl8: t->n_ext * 256 entries). */
+void cop_lpm_fill_dir24(const cop_lpm_table *t, uint32_t *tbl24, uint32_t *tbl8);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,79 @@
+// cop_kernels.h — launch parameters shared by the HIP runtime and the
+// pipeline kernel. Internal (not part of the C ABI).
+#ifndef COP_KERNELS_H
+#define COP_KERNELS_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define COPK_BLOCK 256
+#define COPK_MAXB 32
+
+#define COPK_TBL_OFF 0
+#define COPK_TBL_IVT 1  /* flattened intervals, binary search in LDS */
+#define COPK_TBL_DIR 2  /* DIR-24-8 image in HBM */
+
+#define COPK_STAGE_PARSE 0x1u
+
+#define COPK_FORWARD 0u
+#define COPK_DROP_FW 1u
+#define COPK_DROP_PARSE 2u
+#define COPK_DROP_NOT_IPV4 3u
+#define COPK_DROP_NO_PORT 4u
+#define COPK_FLAG_ROUTE_HIT 0x1u
+#define COPK_FLAG_FW_HIT 0x2u
+
+struct CopKBatch {
+    const uint8_t *pkts;
+    const uint32_t *offsets;
+    void *results;            // uint2 per packet
+    uint32_t *fwd_idx;
+    uint32_t *fwd_count;
+    uint32_t n;
+    uint32_t stride;
+    uint32_t data_off;
+    uint32_t tile_begin;      // first launch-relative tile of this batch
+    uint32_t ntiles;
+    uint32_t _pad;
+};
+
+struct CopKParams {
+    CopKBatch b[COPK_MAXB];
+    uint32_t nb;
+    uint32_t ntiles;
+    uint32_t stages;
+    uint32_t n_ports;
+    uint32_t compact;
+    uint32_t epoch;
+    // vport routing table (two-level image)
+    const uint32_t *rt_top;   // 256 entries: value, or 0x80000000|leaf
+    const uint16_t *rt_leaf;  // nleaf * 256
+    uint32_t rt_nleaf;
+    // firewall LPM
+    uint32_t fw_m;
+    const uint32_t *fw_starts, *fw_vals;
+    const uint32_t *fw_tbl24, *fw_tbl8;
+    // route LPM
+    uint32_t lpm_m;
+    const uint32_t *lpm_starts, *lpm_vals;
+    const uint32_t *lpm_tbl24, *lpm_tbl8;
+    // LDS carve (u32 words)
+    uint32_t lds_fw_off, lds_lpm_off, lds_misc_off;
+    // ordering / accounting state
+    unsigned long long *ticket;
+    unsigned long long ticket_base;
+    unsigned long long *look;
+    unsigned long long *counters;
+    uint32_t *err;
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int imix, int ppt,
+                       uint32_t grid, uint32_t lds_bytes, hipStream_t stream);
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,685 @@
+// cop_runtime.cpp — GPU context behind the C ABI (include/cop_gpu.h).
+//
+// One context = one HIP device + one in-order stream + the device copies of
+// the NF tables. It replaces the process-global NF state of the reference
+// (lpm_tbl / rules / stats globals, firewall.h:107-110, shared and raced by
+// the five coprocessor threads) with per-context state: one context per
+// coprocessor thread or per GPU, no globals.
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "cop_gpu.h"
+#include "cop_internal.h"
+#include "cop_kernels.h"
+
+namespace {
+
+constexpr uint32_t IVT_MAX = 8192;          // LDS interval entries per table (64 KiB)
+constexpr uint32_t LOOK_TILE_MIN = COPK_BLOCK;
+constexpr int TIMING_SLOTS = 1024;
+
+struct DevLpm {
+    bool loaded = false;
+    uint32_t m = 0;                 // padded interval count (power of two) or 0
+    uint32_t *starts = nullptr, *vals = nullptr;
+    uint32_t *tbl24 = nullptr, *tbl8 = nullptr;
+    uint32_t n_ext = 0;
+};
+
+}  // namespace
+
+struct cop_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    cop_config cfg{};
+    int ncu = 256;
+    char err[256] = {0};
+
+    uint32_t *rt_top = nullptr;
+    uint16_t *rt_leaf = nullptr;
+    uint32_t rt_nleaf = 0;
+    DevLpm fw, lpm;
+
+    unsigned long long *ticket = nullptr;
+    unsigned long long ticket_base = 0;
+    unsigned long long *look = nullptr;
+    uint32_t look_cap = 0;
+    uint32_t epoch = 0;
+    unsigned long long *counters = nullptr;     // owned
+    unsigned long long *counters_ext = nullptr; // caller-provided (unused now)
+    uint32_t *h_err = nullptr;                  // host-mapped
+    uint32_t *d_err = nullptr;
+
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    bool timing = false;
+    hipEvent_t ev[TIMING_SLOTS][2];
+    int ev_head = 0, ev_count = 0, ev_created = 0;
+    double ev_sum_ms = 0;
+    uint64_t ev_n = 0;
+
+    // host path staging
+    uint8_t *h_stage = nullptr;
+    uint8_t *d_stage = nullptr;
+    cop_result *d_res = nullptr;
+    uint32_t *d_fwd = nullptr;
+    uint32_t *d_fwdn = nullptr;
+    uint32_t stage_cap = 0;
+};
+
+static int set_err(cop_ctx *c, int code, const char *fmt, ...)
+{
+    if (c) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(c->err, sizeof(c->err), fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                         \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return set_err((c), -EIO, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                           __LINE__);                                                           \
+    } while (0)
+
+static inline uint32_t next_pow2(uint32_t x)
+{
+    uint32_t m = 1;
+    while (m < x) m <<= 1;
+    return m;
+}
+
+extern "C" {
+
+void cop_config_default(cop_config *cfg)
+{
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->device = 0;
+    cfg->stages = COP_DEFAULT_STAGES;
+    cfg->n_ports = COP_KNI_KTHREAD;
+    cfg->max_batch = 262144;
+    cfg->max_batches = COPK_MAXB;
+    cfg->flags = 0;
+    cfg->routing_table = nullptr;
+}
+
+int cop_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char *cop_last_error(cop_ctx *ctx) { return ctx ? ctx->err : "no context"; }
+
+static void free_lpm(DevLpm &t)
+{
+    if (t.starts) (void)hipFree(t.starts);
+    if (t.vals) (void)hipFree(t.vals);
+    if (t.tbl24) (void)hipFree(t.tbl24);
+    if (t.tbl8) (void)hipFree(t.tbl8);
+    t = DevLpm();
+}
+
+void cop_destroy(cop_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_lpm(c->fw);
+    free_lpm(c->lpm);
+    if (c->rt_top) (void)hipFree(c->rt_top);
+    if (c->rt_leaf) (void)hipFree(c->rt_leaf);
+    if (c->ticket) (void)hipFree(c->ticket);
+    if (c->look) (void)hipFree(c->look);
+    if (c->counters) (void)hipFree(c->counters);
+    if (c->h_err) (void)hipHostFree(c->h_err);
+    if (c->t0) (void)hipEventDestroy(c->t0);
+    if (c->t1) (void)hipEventDestroy(c->t1);
+    for (int i = 0; i < c->ev_created; i++) {
+        (void)hipEventDestroy(c->ev[i][0]);
+        (void)hipEventDestroy(c->ev[i][1]);
+    }
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->d_res) (void)hipFree(c->d_res);
+    if (c->d_fwd) (void)hipFree(c->d_fwd);
+    if (c->d_fwdn) (void)hipFree(c->d_fwdn);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int upload_empty_ivt(cop_ctx *c, DevLpm &t)
+{
+    const uint32_t zero4[4] = {0, 0, 0, 0};
+    // m = 4 so the LDS copy works in uint4 units; starts[1..3] = 0xFFFFFFFF
+    // would break the search, so repeat starts 0 with value 0 (same function)
+    free_lpm(t);
+    HIPCHK(c, hipMalloc(&t.starts, 16));
+    HIPCHK(c, hipMalloc(&t.vals, 16));
+    HIPCHK(c, hipMemcpy(t.starts, zero4, 16, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(t.vals, zero4, 16, hipMemcpyHostToDevice));
+    t.m = 4;
+    t.loaded = true;
+    return 0;
+}
+
+int cop_set_routing_table(cop_ctx *c, const uint16_t *rt)
+{
+    if (!c || !rt) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t top[256];
+    std::vector<uint16_t> leaves;
+    uint32_t nleaf = 0;
+    for (uint32_t b = 0; b < 256; b++) {
+        const uint16_t *blk = rt + b * 256;
+        bool uni = true;
+        for (int i = 1; i < 256 && uni; i++) uni = blk[i] == blk[0];
+        if (uni) {
+            top[b] = blk[0];
+        } else {
+            top[b] = 0x80000000u | nleaf;
+            leaves.insert(leaves.end(), blk, blk + 256);
+            nleaf++;
+        }
+    }
+    if (c->rt_top) (void)hipFree(c->rt_top);
+    if (c->rt_leaf) (void)hipFree(c->rt_leaf);
+    c->rt_top = nullptr;
+    c->rt_leaf = nullptr;
+    HIPCHK(c, hipMalloc(&c->rt_top, sizeof(top)));
+    HIPCHK(c, hipMemcpy(c->rt_top, top, sizeof(top), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMalloc(&c->rt_leaf, nleaf ? nleaf * 512 : 16));
+    if (nleaf) HIPCHK(c, hipMemcpy(c->rt_leaf, leaves.data(), nleaf * 512, hipMemcpyHostToDevice));
+    c->rt_nleaf = nleaf;
+    return 0;
+}
+
+int cop_create(const cop_config *cfg_in, cop_ctx **out)
+{
+    if (!out) return -EINVAL;
+    *out = nullptr;
+    cop_config cfg;
+    if (cfg_in) cfg = *cfg_in;
+    else cop_config_default(&cfg);
+    if (cfg.max_batches == 0 || cfg.max_batches > COPK_MAXB || cfg.max_batch == 0 ||
+        cfg.max_batch > (1u << 30) || cfg.n_ports == 0 || cfg.n_ports > 0xFFFFu)
+        return -EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
+    if (cfg.device < 0 || cfg.device >= ndev) return -ENODEV;
+
+    cop_ctx *c = new (std::nothrow) cop_ctx();
+    if (!c) return -ENOMEM;
+    c->device = cfg.device;
+    c->cfg = cfg;
+    c->cfg.routing_table = nullptr;
+    int rc = 0;
+#define CREATE_CHK(expr)                                                                  \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            fprintf(stderr, "cop_create: %s: %s\n", #expr, hipGetErrorString(e_));        \
+            cop_destroy(c);                                                               \
+            return -EIO;                                                                  \
+        }                                                                                 \
+    } while (0)
+    CREATE_CHK(hipSetDevice(c->device));
+    hipDeviceProp_t prop;
+    CREATE_CHK(hipGetDeviceProperties(&prop, c->device));
+    c->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    CREATE_CHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    CREATE_CHK(hipMalloc(&c->ticket, sizeof(unsigned long long)));
+    CREATE_CHK(hipMemset(c->ticket, 0, sizeof(unsigned long long)));
+    uint32_t tiles_per_batch = (cfg.max_batch + LOOK_TILE_MIN - 1) / LOOK_TILE_MIN;
+    c->look_cap = tiles_per_batch * cfg.max_batches;
+    CREATE_CHK(hipMalloc(&c->look, (size_t)c->look_cap * 8));
+    CREATE_CHK(hipMemset(c->look, 0, (size_t)c->look_cap * 8));
+    CREATE_CHK(hipMalloc(&c->counters, COP_N_COUNTERS * 8));
+    CREATE_CHK(hipMemset(c->counters, 0, COP_N_COUNTERS * 8));
+    CREATE_CHK(hipHostMalloc(&c->h_err, 64, hipHostMallocMapped));
+    c->h_err[0] = 0;
+    CREATE_CHK(hipHostGetDevicePointer((void **)&c->d_err, c->h_err, 0));
+    CREATE_CHK(hipEventCreate(&c->t0));
+    CREATE_CHK(hipEventCreate(&c->t1));
+    for (int i = 0; i < TIMING_SLOTS; i++) {
+        CREATE_CHK(hipEventCreate(&c->ev[i][0]));
+        if (hipEventCreate(&c->ev[i][1]) != hipSuccess) {
+            (void)hipEventDestroy(c->ev[i][0]);
+            cop_destroy(c);
+            return -EIO;
+        }
+        c->ev_created = i + 1;
+    }
+    c->ev_count = 0;
+#undef CREATE_CHK
+    uint16_t *rt = (uint16_t *)malloc(COP_ROUTING_TBL_SZ * sizeof(uint16_t));
+    if (!rt) {
+        cop_destroy(c);
+        return -ENOMEM;
+    }
+    if (cfg_in && cfg_in->routing_table) memcpy(rt, cfg_in->routing_table, COP_ROUTING_TBL_SZ * 2);
+    else cop_route_table_default(rt, cfg.n_ports);
+    rc = cop_set_routing_table(c, rt);
+    free(rt);
+    if (!rc) rc = upload_empty_ivt(c, c->fw);
+    if (!rc) rc = upload_empty_ivt(c, c->lpm);
+    if (rc) {
+        fprintf(stderr, "cop_create: %s\n", c->err);
+        cop_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return 0;
+}
+
+static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt)
+{
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    free_lpm(t);
+    // interval form for LDS
+    uint32_t *s = nullptr, *v = nullptr;
+    uint32_t m = cop_lpm_merged_intervals(tab, &s, &v);
+    if (!s) return set_err(c, -ENOMEM, "interval export failed");
+    if (want_ivt && m <= IVT_MAX) {
+        uint32_t M = next_pow2(m < 4 ? 4 : m);
+        std::vector<uint32_t> hs(M), hv(M);
+        for (uint32_t k = 0; k < M; k++) {
+            if (k < m) {
+                hs[k] = s[k];
+                hv[k] = v[k];
+            } else {
+                hs[k] = 0xFFFFFFFFu;
+                hv[k] = v[m - 1];
+            }
+        }
+        // entries past the real ones must never win: start 0xFFFFFFFF only
+        // matches ip 0xFFFFFFFF, whose value equals the last real interval
+        HIPCHK(c, hipMalloc(&t.starts, M * 4));
+        HIPCHK(c, hipMalloc(&t.vals, M * 4));
+        HIPCHK(c, hipMemcpy(t.starts, hs.data(), M * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(t.vals, hv.data(), M * 4, hipMemcpyHostToDevice));
+        t.m = M;
+    }
+    free(s);
+    free(v);
+    // DIR-24-8 image (always: FORCE_DIR24 and the large-table path)
+    std::vector<uint32_t> h24((size_t)1 << 24);
+    std::vector<uint32_t> h8((size_t)(tab->n_ext ? tab->n_ext : 1) * 256);
+    cop_lpm_fill_dir24(tab, h24.data(), h8.data());
+    HIPCHK(c, hipMalloc(&t.tbl24, h24.size() * 4));
+    HIPCHK(c, hipMalloc(&t.tbl8, h8.size() * 4));
+    HIPCHK(c, hipMemcpy(t.tbl24, h24.data(), h24.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(t.tbl8, h8.data(), h8.size() * 4, hipMemcpyHostToDevice));
+    t.n_ext = tab->n_ext;
+    t.loaded = true;
+    return 0;
+}
+
+int cop_set_fw_table(cop_ctx *c, const cop_lpm_table *t)
+{
+    if (!c || !t) return -EINVAL;
+    return upload_lpm(c, c->fw, t, !(c->cfg.flags & COP_CFG_FW_FORCE_DIR24));
+}
+
+int cop_set_route_lpm(cop_ctx *c, const cop_lpm_table *t)
+{
+    if (!c || !t) return -EINVAL;
+    return upload_lpm(c, c->lpm, t, !(c->cfg.flags & COP_CFG_LPM_FORCE_DIR24));
+}
+
+int cop_load_fw_rules_file(cop_ctx *c, const char *path, const cop_lpm_config *cfg,
+                           cop_lpm_report *report)
+{
+    cop_prefix *rules = nullptr;
+    uint32_t n = 0;
+    int rc = cop_rules_load_json(path, &rules, &n);
+    if (rc) return set_err(c, rc, "rules file %s: error %d", path ? path : "(null)", rc);
+    cop_lpm_table *t = nullptr;
+    rc = cop_lpm_build(rules, n, cfg, &t, report);
+    cop_rules_free(rules);
+    if (rc) return set_err(c, rc, "lpm build failed: %d", rc);
+    rc = cop_set_fw_table(c, t);
+    cop_lpm_free(t);
+    return rc;
+}
+
+static int pick_mode(const cop_ctx *c, const DevLpm &t, bool enabled, bool force_dir)
+{
+    if (!enabled) return COPK_TBL_OFF;
+    if (!force_dir && t.m) return COPK_TBL_IVT;
+    if (t.tbl24) return COPK_TBL_DIR;
+    return COPK_TBL_IVT;  // empty table (m = 4)
+}
+
+static void harvest_one(cop_ctx *c)
+{
+    int idx = (c->ev_head - c->ev_count + TIMING_SLOTS) % TIMING_SLOTS;
+    float ms = 0;
+    if (hipEventSynchronize(c->ev[idx][1]) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->ev[idx][0], c->ev[idx][1]) == hipSuccess) {
+        c->ev_sum_ms += ms;
+        c->ev_n++;
+    }
+    c->ev_count--;
+}
+
+int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
+{
+    if (!c || (!batches && nb)) return -EINVAL;
+    if (nb == 0) return 0;
+    if (nb > c->cfg.max_batches) return set_err(c, -EINVAL, "nb %u > max_batches", nb);
+    const uint32_t stages = c->cfg.stages;
+    const bool fw_on = (stages & COP_STAGE_FW) != 0;
+    const bool lpm_on = (stages & COP_STAGE_LPM) != 0;
+    int fw_mode = pick_mode(c, c->fw, fw_on, (c->cfg.flags & COP_CFG_FW_FORCE_DIR24) != 0);
+    int lpm_mode = pick_mode(c, c->lpm, lpm_on, (c->cfg.flags & COP_CFG_LPM_FORCE_DIR24) != 0);
+
+    CopKParams p;
+    memset(&p, 0, sizeof(p));
+    uint64_t total = 0;
+    bool imix = batches[0].offsets != nullptr;
+    bool compact = false;
+    for (uint32_t i = 0; i < nb; i++) {
+        const cop_batch &b = batches[i];
+        if ((b.offsets != nullptr) != imix)
+            return set_err(c, -EINVAL, "batches in one submit must all be slot or all IMIX");
+        if (b.n > c->cfg.max_batch) return set_err(c, -EINVAL, "batch %u: n %u > max_batch", i, b.n);
+        if (b.n && (!b.pkts || !b.results)) return set_err(c, -EINVAL, "batch %u: null pointer", i);
+        if (((uintptr_t)b.pkts & 15) || (b.data_off & 15) || (!imix && (b.stride & 15)) ||
+            (!imix && b.stride < 36))
+            return set_err(c, -EINVAL, "batch %u: packet starts must be 16-byte aligned", i);
+        if ((uintptr_t)b.results & 7) return set_err(c, -EINVAL, "batch %u: results misaligned", i);
+        total += b.n;
+        if (b.fwd_idx || b.fwd_count) compact = true;
+    }
+    if (c->cfg.flags & COP_CFG_NO_COMPACT) compact = false;
+    // tile size: 1024 packets when there is enough work for >= 2 tiles per CU
+    const int ppt = (total >= (uint64_t)COPK_BLOCK * 4 * 2 * c->ncu) ? 4 : 1;
+    const uint32_t tile = COPK_BLOCK * ppt;
+    uint32_t ntiles = 0;
+    for (uint32_t i = 0; i < nb; i++) {
+        const cop_batch &b = batches[i];
+        CopKBatch &d = p.b[i];
+        d.pkts = (const uint8_t *)b.pkts;
+        d.offsets = b.offsets;
+        d.results = b.results;
+        d.fwd_idx = compact ? b.fwd_idx : nullptr;
+        d.fwd_count = compact ? b.fwd_count : nullptr;
+        d.n = b.n;
+        d.stride = b.stride;
+        d.data_off = b.data_off;
+        d.tile_begin = ntiles;
+        d.ntiles = b.n ? (b.n + tile - 1) / tile : 1;   // an empty batch still reports count 0
+        ntiles += d.ntiles;
+    }
+    if (ntiles > c->look_cap) return set_err(c, -EINVAL, "too many tiles");
+    p.nb = nb;
+    p.ntiles = ntiles;
+    p.stages = stages;
+    p.n_ports = c->cfg.n_ports;
+    p.compact = compact ? 1u : 0u;
+    if (++c->epoch == 0) {
+        HIPCHK(c, hipMemsetAsync(c->look, 0, (size_t)c->look_cap * 8, c->stream));
+        c->epoch = 1;
+    }
+    p.epoch = c->epoch;
+    p.rt_top = c->rt_top;
+    p.rt_leaf = c->rt_leaf;
+    p.rt_nleaf = c->rt_nleaf;
+    p.fw_m = fw_mode == COPK_TBL_IVT ? c->fw.m : 0;
+    p.fw_starts = c->fw.starts;
+    p.fw_vals = c->fw.vals;
+    p.fw_tbl24 = c->fw.tbl24;
+    p.fw_tbl8 = c->fw.tbl8;
+    p.lpm_m = lpm_mode == COPK_TBL_IVT ? c->lpm.m : 0;
+    p.lpm_starts = c->lpm.starts;
+    p.lpm_vals = c->lpm.vals;
+    p.lpm_tbl24 = c->lpm.tbl24;
+    p.lpm_tbl8 = c->lpm.tbl8;
+    // LDS carve (u32 words): rt_top 256 | leaves nleaf*128 | fw 2m | lpm 2m | misc
+    uint32_t off = 256 + c->rt_nleaf * 128;
+    p.lds_fw_off = off;
+    off += 2 * p.fw_m;
+    p.lds_lpm_off = off;
+    off += 2 * p.lpm_m;
+    p.lds_misc_off = off;
+    off += 4 * 4 + 8;
+    const uint32_t lds_bytes = off * 4;
+    if (lds_bytes > 160 * 1024) return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_bytes);
+    p.ticket = c->ticket;
+    p.ticket_base = c->ticket_base;
+    p.look = c->look;
+    p.counters = c->counters;
+    p.err = c->d_err;
+
+    uint32_t per_cu = (160u * 1024u) / (lds_bytes < 1024 ? 1024 : lds_bytes);
+    if (per_cu > 8) per_cu = 8;
+    if (per_cu < 1) per_cu = 1;
+    uint32_t grid = (uint32_t)c->ncu * per_cu;
+    if (grid > ntiles) grid = ntiles;
+    c->ticket_base += (unsigned long long)ntiles + grid;
+
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->timing) {
+        if (c->ev_count == TIMING_SLOTS) harvest_one(c);
+        HIPCHK(c, hipEventRecord(c->ev[c->ev_head][0], c->stream));
+    }
+    hipError_t e = copk_launch(&p, fw_mode, lpm_mode, imix ? 1 : 0, ppt, grid, lds_bytes, c->stream);
+    if (e != hipSuccess) {
+        c->ticket_base -= (unsigned long long)ntiles + grid;
+        return set_err(c, -EIO, "launch: %s", hipGetErrorString(e));
+    }
+    if (c->timing) {
+        HIPCHK(c, hipEventRecord(c->ev[c->ev_head][1], c->stream));
+        c->ev_head = (c->ev_head + 1) % TIMING_SLOTS;
+        c->ev_count++;
+    }
+    return 0;
+}
+
+int cop_sync(cop_ctx *c)
+{
+    if (!c) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->h_err[0]) {
+        c->h_err[0] = 0;
+        return set_err(c, -EIO, "device reported a look-back timeout");
+    }
+    return 0;
+}
+
+int cop_poll(cop_ctx *c)
+{
+    if (!c) return -EINVAL;
+    hipError_t e = hipStreamQuery(c->stream);
+    if (e == hipErrorNotReady) return -EAGAIN;
+    if (e != hipSuccess) return set_err(c, -EIO, "stream: %s", hipGetErrorString(e));
+    if (c->h_err[0]) {
+        c->h_err[0] = 0;
+        return set_err(c, -EIO, "device reported a look-back timeout");
+    }
+    return 0;
+}
+
+int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_result *results,
+                     uint32_t *fwd_idx, uint32_t *fwd_count)
+{
+    if (!c || (n && (!pkt_data || !results))) return -EINVAL;
+    if (n > c->cfg.max_batch) return set_err(c, -EINVAL, "n %u > max_batch", n);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->stage_cap < n || !c->h_stage) {
+        uint32_t cap = n < 1024 ? 1024 : n;
+        if (c->h_stage) (void)hipHostFree(c->h_stage);
+        if (c->d_stage) (void)hipFree(c->d_stage);
+        if (c->d_res) (void)hipFree(c->d_res);
+        if (c->d_fwd) (void)hipFree(c->d_fwd);
+        if (c->d_fwdn) (void)hipFree(c->d_fwdn);
+        c->h_stage = nullptr;
+        c->d_stage = nullptr;
+        c->d_res = nullptr;
+        c->d_fwd = nullptr;
+        c->d_fwdn = nullptr;
+        c->stage_cap = 0;
+        HIPCHK(c, hipHostMalloc(&c->h_stage, (size_t)cap * 64, hipHostMallocDefault));
+        HIPCHK(c, hipMalloc(&c->d_stage, (size_t)cap * 64));
+        HIPCHK(c, hipMalloc(&c->d_res, (size_t)cap * 8));
+        HIPCHK(c, hipMalloc(&c->d_fwd, (size_t)cap * 4));
+        HIPCHK(c, hipMalloc(&c->d_fwdn, 16));
+        c->stage_cap = cap;
+    }
+    // gather the first 64 bytes of every packet (headers the pipeline reads)
+    for (uint32_t i = 0; i < n; i++) memcpy(c->h_stage + (size_t)i * 64, pkt_data[i], 64);
+    HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, (size_t)n * 64, hipMemcpyHostToDevice, c->stream));
+    cop_batch b;
+    memset(&b, 0, sizeof(b));
+    b.pkts = c->d_stage;
+    b.n = n;
+    b.stride = 64;
+    b.results = c->d_res;
+    b.fwd_idx = fwd_idx ? c->d_fwd : nullptr;
+    b.fwd_count = (fwd_idx || fwd_count) ? c->d_fwdn : nullptr;
+    int rc = cop_submit(c, &b, 1);
+    if (rc) return rc;
+    HIPCHK(c, hipMemcpyAsync(results, c->d_res, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    uint32_t cnt = 0;
+    if (b.fwd_count) {
+        HIPCHK(c, hipMemcpyAsync(&cnt, c->d_fwdn, 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    rc = cop_sync(c);
+    if (rc) return rc;
+    if (fwd_idx && cnt) HIPCHK(c, hipMemcpy(fwd_idx, c->d_fwd, (size_t)cnt * 4, hipMemcpyDeviceToHost));
+    if (fwd_count) *fwd_count = cnt;
+    return 0;
+}
+
+int cop_counters_read(cop_ctx *c, cop_counters *out, int reset)
+{
+    if (!c || !out) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, c->counters, sizeof(cop_counters), hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(c, hipMemset(c->counters, 0, sizeof(cop_counters)));
+    return 0;
+}
+
+void *cop_counters_device_ptr(cop_ctx *c) { return c ? (void *)c->counters : nullptr; }
+
+int cop_dev_alloc(cop_ctx *c, size_t bytes, void **dptr)
+{
+    if (!c || !dptr) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMalloc(dptr, bytes ? bytes : 16));
+    return 0;
+}
+
+int cop_dev_free(cop_ctx *c, void *dptr)
+{
+    if (!c) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipFree(dptr));
+    return 0;
+}
+
+int cop_host_alloc_pinned(cop_ctx *c, size_t bytes, void **hptr)
+{
+    if (!c || !hptr) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocDefault));
+    return 0;
+}
+
+int cop_host_free_pinned(cop_ctx *c, void *hptr)
+{
+    if (!c) return -EINVAL;
+    HIPCHK(c, hipHostFree(hptr));
+    return 0;
+}
+
+int cop_memcpy_h2d(cop_ctx *c, void *dst, const void *src, size_t bytes)
+{
+    if (!c) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int cop_memcpy_d2h(cop_ctx *c, void *dst, const void *src, size_t bytes)
+{
+    if (!c) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int cop_memcpy_d2d(cop_ctx *c, void *dst, const void *src, size_t bytes)
+{
+    if (!c) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int cop_memset_d(cop_ctx *c, void *dst, int value, size_t bytes)
+{
+    if (!c) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemsetAsync(dst, value, bytes, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int cop_timer_start(cop_ctx *c)
+{
+    if (!c) return -EINVAL;
+    HIPCHK(c, hipEventRecord(c->t0, c->stream));
+    return 0;
+}
+
+int cop_timer_stop(cop_ctx *c, double *ms)
+{
+    if (!c || !ms) return -EINVAL;
+    HIPCHK(c, hipEventRecord(c->t1, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->t1));
+    float f = 0;
+    HIPCHK(c, hipEventElapsedTime(&f, c->t0, c->t1));
+    *ms = f;
+    return 0;
+}
+
+int cop_launch_timing(cop_ctx *c, int enable)
+{
+    if (!c) return -EINVAL;
+    c->timing = enable != 0;
+    return 0;
+}
+
+int cop_launch_timing_read(cop_ctx *c, double *mean_ms, uint64_t *n, int reset)
+{
+    if (!c) return -EINVAL;
+    while (c->ev_count) harvest_one(c);
+    if (mean_ms) *mean_ms = c->ev_n ? c->ev_sum_ms / (double)c->ev_n : 0.0;
+    if (n) *n = c->ev_n;
+    if (reset) {
+        c->ev_sum_ms = 0;
+        c->ev_n = 0;
+    }
+    return 0;
+}
+
+}  // extern "C"

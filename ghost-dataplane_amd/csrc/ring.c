@@ -1,0 +1,86 @@
+/*
+ * ring.c — single-producer / single-consumer descriptor ring with the
+ * rte_ring semantics the reference relies on:
+ *   rte_ring_create(name, 16384, socket, RING_F_SC_DEQ)   init.c:74-75
+ *     power-of-two size, usable capacity size-1 (no RING_F_EXACT_SZ);
+ *   rte_ring_enqueue_bulk(r, objs, n, NULL)                switch.c:225,268
+ *     all-or-nothing, returns n or 0;
+ *   rte_ring_dequeue_burst(r, objs, n, NULL)               switch.c:430,463
+ *     returns up to n.
+ * In the reference each ring has exactly one producer thread and one
+ * consumer thread (the fast path and one coprocessor), so SPSC with
+ * acquire/release ordering is the whole contract.
+ */
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "cop_gpu.h"
+
+struct cop_ring {
+    _Alignas(64) _Atomic uint32_t prod;  /* written by the producer */
+    _Alignas(64) _Atomic uint32_t cons;  /* written by the consumer */
+    _Alignas(64) uint32_t size, mask, capacity;
+    void **slots;
+};
+
+cop_ring *cop_ring_create(uint32_t count)
+{
+    if (count < 2 || (count & (count - 1))) return NULL;
+    cop_ring *r = (cop_ring *)aligned_alloc(64, sizeof(cop_ring));
+    if (!r) return NULL;
+    memset(r, 0, sizeof(*r));
+    r->slots = (void **)calloc(count, sizeof(void *));
+    if (!r->slots) {
+        free(r);
+        return NULL;
+    }
+    r->size = count;
+    r->mask = count - 1;
+    r->capacity = count - 1;
+    atomic_init(&r->prod, 0);
+    atomic_init(&r->cons, 0);
+    return r;
+}
+
+void cop_ring_free(cop_ring *r)
+{
+    if (!r) return;
+    free(r->slots);
+    free(r);
+}
+
+uint32_t cop_ring_enqueue_bulk(cop_ring *r, void *const *objs, uint32_t n, uint32_t *free_space)
+{
+    uint32_t head = atomic_load_explicit(&r->prod, memory_order_relaxed);
+    uint32_t tail = atomic_load_explicit(&r->cons, memory_order_acquire);
+    uint32_t free_entries = r->capacity - (head - tail);
+    if (n > free_entries) {
+        if (free_space) *free_space = free_entries;
+        return 0;
+    }
+    for (uint32_t i = 0; i < n; i++) r->slots[(head + i) & r->mask] = objs[i];
+    atomic_store_explicit(&r->prod, head + n, memory_order_release);
+    if (free_space) *free_space = free_entries - n;
+    return n;
+}
+
+uint32_t cop_ring_dequeue_burst(cop_ring *r, void **objs, uint32_t n, uint32_t *available)
+{
+    uint32_t head = atomic_load_explicit(&r->cons, memory_order_relaxed);
+    uint32_t tail = atomic_load_explicit(&r->prod, memory_order_acquire);
+    uint32_t entries = tail - head;
+    if (n > entries) n = entries;
+    for (uint32_t i = 0; i < n; i++) objs[i] = r->slots[(head + i) & r->mask];
+    atomic_store_explicit(&r->cons, head + n, memory_order_release);
+    if (available) *available = entries - n;
+    return n;
+}
+
+uint32_t cop_ring_count(const cop_ring *r)
+{
+    cop_ring *rr = (cop_ring *)r;
+    uint32_t tail = atomic_load_explicit(&rr->prod, memory_order_acquire);
+    uint32_t head = atomic_load_explicit(&rr->cons, memory_order_acquire);
+    return tail - head;
+}

@@ -1,0 +1,371 @@
+/*
+ * cop_gpu.h — C-ABI boundary of the MI355X coprocessor NF pipeline.
+ *
+ * This is the drop-in boundary for the per-packet coprocessor path of
+ * google/ghost-dataplane (reference, read-only at /root/reference):
+ *
+ *   engine/switch.c:443-474   coprocessor()        burst loop, forward/free
+ *   engine/coprocessor.c:21-65 coprocessor_setup / coprocessor_teardown /
+ *                              process_packet       (declared coprocessor.h:23-30)
+ *   engine/nfs/firewall/firewall.c:170-213 fw_packet_handler
+ *   engine/nfs/firewall/firewall.c:215-255 lpm_setup (rte_lpm_create/add)
+ *   engine/nfs/firewall/firewall.c:276-323 setup_rules (rules.json loader)
+ *   engine/switch.c:93-136    get_next_hop (parse + vport route)
+ *   engine/init.c:40-84       read_config (routing table defaults)
+ *
+ * Everything here is plain C: pointers, sizes, negative-errno return codes.
+ * No torch, no CUDA-compat headers; HIP is called only inside libcopgpu.so.
+ */
+#ifndef COP_GPU_H
+#define COP_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Constants mirrored from the reference                                    */
+/* ------------------------------------------------------------------------ */
+
+#define COP_UNKNOWN_PORT      0xFFFFu   /* UNKNOWN_PORT       init.h:28 */
+#define COP_ROUTING_TBL_SZ    0x10000u  /* ROUTING_TBL_SZ     init.h:29 */
+#define COP_PKT_BURST_SZ      32u       /* PKT_BURST_SZ       init.h:47 */
+#define COP_KNI_KTHREAD       5u        /* KNI_KTHREAD        init.h:52 */
+#define COP_NF_QUEUE_RINGSIZE 16384u    /* NF_QUEUE_RINGSIZE  init.h:54 */
+#define COP_ETHER_TYPE_IPV4   0x0800u   /* ETHER_TYPE_IPv4    switch.c:118 */
+#define COP_FW_MAX_RULES      1024u     /* conf.max_rules     firewall.c:234 */
+#define COP_FW_NUMBER_TBL8S   24u       /* conf.number_tbl8s  firewall.c:235 */
+#define COP_LPM_MAX_DEPTH     32u       /* RTE_LPM_MAX_DEPTH  (DPDK rte_lpm.h) */
+#define COP_LPM_NH_MASK       0x00FFFFFFu /* 24-bit next hop  (DPDK v1604 ABI) */
+
+/* Stage flags. The reference selects stages at compile time with
+ * ENABLE_FW_NF / DISABLE_NF (coprocessor.h:19-21, switch.c:411,426,524);
+ * the same macro names select COP_DEFAULT_STAGES here, and cop_config.stages
+ * carries the mask to the device at run time. */
+#define COP_STAGE_PARSE 0x1u  /* get_next_hop switch.c:93-136            */
+#define COP_STAGE_FW    0x2u  /* fw_packet_handler firewall.c:170-213    */
+#define COP_STAGE_LPM   0x4u  /* route LPM on dst (north-star extension) */
+
+#if defined(DISABLE_NF)
+#define COP_DEFAULT_STAGES (COP_STAGE_PARSE)
+#elif defined(ENABLE_FW_NF)
+#define COP_DEFAULT_STAGES (COP_STAGE_PARSE | COP_STAGE_FW)
+#else
+#define COP_DEFAULT_STAGES (COP_STAGE_PARSE | COP_STAGE_FW)
+#endif
+
+/* Per-packet verdicts (one byte of the result record).
+ *   FORWARD/DROP_FW : enum FW_ACTION firewall.h:71-74 (FW_FORWARD=0, FW_DROP=1)
+ *   DROP_PARSE      : get_next_hop() == UNKNOWN_PORT, freed by the fast path
+ *                     (switch.c:406-410); never reaches the coprocessor
+ *   DROP_NOT_IPV4   : version nibble != 4. The reference counts it
+ *                     (firewall.c:186-190) and then dereferences NULL at
+ *                     firewall.c:193-194 (undefined behaviour); this build
+ *                     defines the outcome as a drop.
+ *   DROP_NO_PORT    : port >= number of active vports; the reference's
+ *                     enqueue_nf_rx silently discards it (switch.c:316-319). */
+enum cop_verdict {
+    COP_FORWARD       = 0,
+    COP_DROP_FW       = 1,
+    COP_DROP_PARSE    = 2,
+    COP_DROP_NOT_IPV4 = 3,
+    COP_DROP_NO_PORT  = 4
+};
+
+#define COP_FLAG_ROUTE_HIT 0x1u /* route LPM lookup hit (rte_lpm_lookup ret == 0) */
+#define COP_FLAG_FW_HIT    0x2u /* firewall LPM lookup hit                         */
+
+/* 8-byte per-packet result record (SURVEY.md §8a "bit-exact contract"). */
+typedef struct cop_result {
+    uint8_t  verdict;   /* enum cop_verdict */
+    uint8_t  flags;     /* COP_FLAG_* */
+    uint16_t port;      /* vport from the routing table, or COP_UNKNOWN_PORT */
+    uint32_t route_nh;  /* 24-bit next hop of the route LPM stage (0 on miss) */
+} cop_result;
+
+/* One prefix rule: struct fw_rule firewall.h:49-53 ({src_ip, depth, action})
+ * generalised to a 24-bit next hop so the same type carries route prefixes. */
+typedef struct cop_prefix {
+    uint32_t ip;        /* host byte order, unmasked (rte_lpm_add masks it) */
+    uint32_t next_hop;  /* FW: action (uint8 in the reference); routes: 24-bit */
+    uint8_t  depth;     /* 1..32 accepted; anything else is -EINVAL */
+    uint8_t  _pad[3];
+} cop_prefix;
+
+/* rte_lpm_config as used by lpm_setup (firewall.c:229-235). */
+typedef struct cop_lpm_config {
+    uint32_t max_rules;     /* distinct (prefix, depth) rules; default 1024 */
+    uint32_t number_tbl8s;  /* tbl8 groups (/24s holding a depth>24 prefix); default 24 */
+    uint32_t flags;         /* COP_LPM_* */
+} cop_lpm_config;
+
+/* Reproduce lpm_setup's "print, return 1 at the first failed rte_lpm_add"
+ * (firewall.c:245-251): every later rule is dropped. Without this flag a
+ * failed rule is skipped, counted in the report, and loading continues. */
+#define COP_LPM_STOP_AT_FIRST_ERROR 0x1u
+
+typedef struct cop_lpm_report {
+    uint32_t n_in;            /* rules presented */
+    uint32_t n_added;         /* rte_lpm_add calls that returned 0 */
+    uint32_t n_distinct;      /* distinct rules held (rule-table occupancy) */
+    uint32_t n_updated;       /* adds that hit an existing rule (last write wins) */
+    uint32_t n_failed;        /* adds that returned < 0 */
+    uint32_t n_skipped;       /* rules never presented (after a stop-at-first-error) */
+    int32_t  first_error;     /* errno of the first failure (negative) or 0 */
+    uint32_t first_error_idx; /* index of the first failed rule */
+    uint32_t tbl8_used;       /* tbl8 groups in use */
+    uint32_t n_intervals;     /* disjoint address intervals of the flattened table */
+} cop_lpm_report;
+
+/* ------------------------------------------------------------------------ */
+/* Host-side LPM table (build once, upload to every GPU context)            */
+/* ------------------------------------------------------------------------ */
+
+typedef struct cop_lpm_table cop_lpm_table;
+
+/* Build a table with DPDK rte_lpm_add semantics:
+ * depth 1..32 else -EINVAL; ip masked to depth; a duplicate (prefix, depth)
+ * overwrites the next hop; a new rule fails -ENOSPC once max_rules distinct
+ * rules are held, or when it needs a tbl8 group and all number_tbl8s are in
+ * use; a failed add leaves the table unchanged. Returns 0 or -errno. */
+int  cop_lpm_build(const cop_prefix *rules, uint32_t n, const cop_lpm_config *cfg,
+                   cop_lpm_table **out, cop_lpm_report *report);
+void cop_lpm_free(cop_lpm_table *t);
+/* Export the DIR-24-8 image: tbl24 has 1<<24 entries, tbl8 has tbl8_used*256.
+ * Entry layout: bits 0-23 next hop (or tbl8 group), bit 24 valid,
+ * bit 25 valid_group (extended), bits 26-31 depth — the DPDK v1604 layout. */
+int  cop_lpm_export_dir24(const cop_lpm_table *t, uint32_t *tbl24, uint32_t *tbl8,
+                          uint32_t tbl8_cap_entries);
+/* Export the flattened form: starts[k] ascending, starts[0] == 0; value[k] =
+ * (hit << 24) | next_hop for addresses in [starts[k], starts[k+1]). */
+int  cop_lpm_export_intervals(const cop_lpm_table *t, uint32_t *starts, uint32_t *values,
+                              uint32_t cap);
+/* Accepted rule set after all adds: masked prefix, depth, final next hop. */
+int  cop_lpm_export_rules(const cop_lpm_table *t, cop_prefix *out, uint32_t cap);
+
+/* ------------------------------------------------------------------------ */
+/* Rule files (rules.json format, firewall.c:57-105,276-323)                */
+/* ------------------------------------------------------------------------ */
+
+/* Parse a rules file: a JSON object (or array) whose children are objects
+ * with case-insensitive keys "ip" (dotted quad, parsed with the reference's
+ * sscanf("%u.%u.%u.%u") and &0xff per byte), "depth" and "action" (cJSON
+ * valueint truncated to uint8). *out is malloc'd; free with cop_rules_free.
+ * Errors: -ENOENT (open), -EINVAL (syntax, missing key, bad ip). */
+int  cop_rules_load_json(const char *path, cop_prefix **out, uint32_t *n);
+void cop_rules_free(cop_prefix *rules);
+/* Write rules pretty-printed with short lines (<255 chars, firewall.c:72,95). */
+int  cop_rules_write_json(const char *path, const cop_prefix *rules, uint32_t n);
+
+/* Default vport routing table (read_config, init.c:40-84): all 0, entries
+ * 0..n_ports-1 = UNKNOWN_PORT, entry (192.167.10.(i+1) & 0xFFFF) = i. */
+void cop_route_table_default(uint16_t *rt /* COP_ROUTING_TBL_SZ */, uint32_t n_ports);
+
+/* ------------------------------------------------------------------------ */
+/* GPU context: one per coprocessor thread or per GPU                       */
+/* ------------------------------------------------------------------------ */
+
+typedef struct cop_ctx cop_ctx;
+
+#define COP_CFG_FW_FORCE_DIR24  0x1u  /* FW lookups from the HBM DIR-24-8 image, not LDS */
+#define COP_CFG_LPM_FORCE_DIR24 0x2u  /* route lookups from HBM even if small */
+#define COP_CFG_NO_COMPACT      0x4u  /* never build the ordered forward list */
+
+typedef struct cop_config {
+    int      device;          /* HIP device ordinal */
+    uint32_t stages;          /* COP_STAGE_* mask */
+    uint32_t n_ports;         /* nb_active_kni (init.c:63), default 5 */
+    uint32_t max_batch;       /* packets per batch, default 262144 */
+    uint32_t max_batches;     /* batches per cop_submit, default 32 */
+    uint32_t flags;           /* COP_CFG_* */
+    const uint16_t *routing_table; /* 65536 entries, or NULL = read_config default */
+} cop_config;
+
+void cop_config_default(cop_config *cfg);
+
+/* Returns 0 or -ENODEV (no GPU), -EINVAL, -ENOMEM, -EIO (HIP error). */
+int  cop_create(const cop_config *cfg, cop_ctx **out);
+void cop_destroy(cop_ctx *ctx);
+const char *cop_last_error(cop_ctx *ctx);
+int  cop_device_count(void);
+
+/* Upload tables (synchronous). The table may be freed afterwards. */
+int  cop_set_fw_table(cop_ctx *ctx, const cop_lpm_table *t);
+int  cop_set_route_lpm(cop_ctx *ctx, const cop_lpm_table *t);
+int  cop_set_routing_table(cop_ctx *ctx, const uint16_t *rt /* 65536 */);
+/* setup_rules + lpm_setup in one call: read a rules.json file and build the
+ * firewall table with cfg (NULL = reference 1024/24, stop at first error). */
+int  cop_load_fw_rules_file(cop_ctx *ctx, const char *path, const cop_lpm_config *cfg,
+                            cop_lpm_report *report);
+
+/* One batch of packets resident in device memory (HBM).
+ * Packet i starts at  pkts + (offsets ? offsets[i] : i * stride) + data_off.
+ * Every packet start must be 16-byte aligned and hold >= 34 readable bytes
+ * (Ethernet + IPv4 header, fixed offsets as firewall.c:143-145 /
+ * switch.c:125-127 read them). Outputs: results[i] for every packet;
+ * fwd_idx[0..*fwd_count) = indices of FORWARD packets in arrival order (the
+ * order coprocessor() enqueues them to tx_q, switch.c:464-470). */
+typedef struct cop_batch {
+    const void     *pkts;      /* device pointer */
+    const uint32_t *offsets;   /* device pointer or NULL (IMIX slab mode) */
+    uint32_t        n;         /* packets */
+    uint32_t        stride;    /* bytes between packet slots (no offsets) */
+    uint32_t        data_off;  /* added to every packet start (mbuf headroom) */
+    uint32_t        _pad;
+    cop_result     *results;   /* device pointer, n records */
+    uint32_t       *fwd_idx;   /* device pointer, n entries, or NULL */
+    uint32_t       *fwd_count; /* device pointer, 1 entry, or NULL */
+} cop_batch;
+
+/* Enqueue nb batches (nb <= max_batches) as ONE kernel launch on the
+ * context's stream. Asynchronous: returns after the launch is queued. */
+int  cop_submit(cop_ctx *ctx, const cop_batch *batches, uint32_t nb);
+/* Block until everything submitted has completed. 0 or -EIO. */
+int  cop_sync(cop_ctx *ctx);
+/* Non-blocking: 0 when idle, -EAGAIN while work is in flight. */
+int  cop_poll(cop_ctx *ctx);
+
+/* End-to-end path from host memory (NIC/KNI mbuf data): gather the first 64
+ * bytes of each packet into pinned staging, hipMemcpyAsync H2D, run the
+ * pipeline, hipMemcpyAsync D2H of results and forward list. Synchronous. */
+int  cop_process_host(cop_ctx *ctx, const void *const *pkt_data, uint32_t n,
+                      cop_result *results, uint32_t *fwd_idx, uint32_t *fwd_count);
+
+/* Counters (u64, device-resident, summed over every submitted packet).
+ * pkt_total / pkt_not_ipv4 mirror struct firewall_pkt_stats
+ * (firewall.h:56-61, incremented at firewall.c:184,188); pkt_accept /
+ * pkt_drop are filled here although the reference never increments them. */
+typedef struct cop_counters {
+    uint64_t pkt_drop;       /* DROP_FW + DROP_NOT_IPV4 (FW stage) */
+    uint64_t pkt_accept;     /* FORWARD after the FW stage */
+    uint64_t pkt_not_ipv4;
+    uint64_t pkt_total;      /* packets that entered the FW stage */
+    uint64_t parse_err;      /* DROP_PARSE (kni_interface_stats.parse_err) */
+    uint64_t no_port;        /* DROP_NO_PORT */
+    uint64_t forward;        /* verdict FORWARD (coprocessor tx) */
+    uint64_t route_hit;      /* route LPM hits */
+    uint64_t rx;             /* packets submitted */
+    uint64_t _rsvd[7];
+} cop_counters;
+#define COP_N_COUNTERS 16
+
+int  cop_counters_read(cop_ctx *ctx, cop_counters *out, int reset);
+/* Device address of the 16 u64 counters (for an RCCL all-reduce in place). */
+void *cop_counters_device_ptr(cop_ctx *ctx);
+
+/* Device memory helpers so C callers need no HIP headers. */
+int  cop_dev_alloc(cop_ctx *ctx, size_t bytes, void **dptr);
+int  cop_dev_free(cop_ctx *ctx, void *dptr);
+int  cop_host_alloc_pinned(cop_ctx *ctx, size_t bytes, void **hptr);
+int  cop_host_free_pinned(cop_ctx *ctx, void *hptr);
+int  cop_memcpy_h2d(cop_ctx *ctx, void *dst, const void *src, size_t bytes);
+int  cop_memcpy_d2h(cop_ctx *ctx, void *dst, const void *src, size_t bytes);
+int  cop_memcpy_d2d(cop_ctx *ctx, void *dst, const void *src, size_t bytes);
+int  cop_memset_d(cop_ctx *ctx, void *dst, int value, size_t bytes);
+
+/* Timing with HIP events on the context's stream. */
+int  cop_timer_start(cop_ctx *ctx);
+int  cop_timer_stop(cop_ctx *ctx, double *ms);
+/* When on, every cop_submit is bracketed by an event pair; the mean kernel
+ * duration of the launches since the last reset is returned in ms. */
+int  cop_launch_timing(cop_ctx *ctx, int enable);
+int  cop_launch_timing_read(cop_ctx *ctx, double *mean_ms, uint64_t *n, int reset);
+
+/* ------------------------------------------------------------------------ */
+/* SPSC ring with rte_ring bulk/burst semantics (init.c:74-75, switch.c)    */
+/* ------------------------------------------------------------------------ */
+
+typedef struct cop_ring cop_ring;
+/* count must be a power of two; capacity is count - 1 (rte_ring default). */
+cop_ring *cop_ring_create(uint32_t count);
+void      cop_ring_free(cop_ring *r);
+/* All-or-nothing: returns n or 0 (rte_ring_enqueue_bulk, switch.c:225,268). */
+uint32_t  cop_ring_enqueue_bulk(cop_ring *r, void *const *objs, uint32_t n, uint32_t *free_space);
+/* Up to n (rte_ring_dequeue_burst, switch.c:430,463). */
+uint32_t  cop_ring_dequeue_burst(cop_ring *r, void **objs, uint32_t n, uint32_t *available);
+uint32_t  cop_ring_count(const cop_ring *r);
+
+/* ------------------------------------------------------------------------ */
+/* Drop-in coprocessor API (coprocessor.h:23-30)                            */
+/* ------------------------------------------------------------------------ */
+
+/* rte_mbuf is opaque; the packet data address is
+ * *(void **)(m + buf_addr_off) + *(uint16_t *)(m + data_off_off)
+ * (rte_pktmbuf_mtod). Defaults match DPDK 17.11-19.05: 0 and 16. */
+struct rte_mbuf;
+void cop_set_mbuf_layout(uint32_t buf_addr_off, uint32_t data_off_off);
+/* Rule file used by coprocessor_setup (coprocessor.c:19); default
+ * "./nfs/firewall/rules.json", or $COP_RULE_FILE when set. */
+void cop_set_rule_file(const char *path);
+
+/* Per calling thread: create a GPU context (device = $COP_DEVICE or 0),
+ * load the rule file with the reference limits. 0 or non-zero. */
+int coprocessor_setup(void);
+int coprocessor_teardown(void);
+/* 0 = forward, -1 = drop (coprocessor.c:50-65). One-packet GPU batch:
+ * correct but latency-bound; use process_burst / cop_coprocessor_poll. */
+int process_packet(struct rte_mbuf *pkt);
+/* Burst form: ret[i] = process_packet(pkts[i]) for all i, one GPU batch. */
+int process_burst(struct rte_mbuf **pkts, uint32_t n, int *ret);
+
+/* Per-coprocessor counters (struct coprocessor_stats, switch.h:33-38). */
+typedef struct cop_nf_stats {
+    uint64_t rx_packets;
+    uint64_t rx_dropped;
+    uint64_t tx_packets;
+    uint64_t tx_dropped;
+} cop_nf_stats;
+
+/* GPU replacement for one call of coprocessor() (switch.c:443-474): drain up
+ * to max_pkts mbufs from rx in bursts of PKT_BURST_SZ, run them as one GPU
+ * batch, enqueue forwarded mbufs to tx in arrival order in bulk bursts of
+ * PKT_BURST_SZ (a burst that does not fit is freed and counted tx_dropped),
+ * and free dropped mbufs with free_fn. Returns packets processed or -errno. */
+typedef void (*cop_free_fn)(struct rte_mbuf *m, void *arg);
+int cop_coprocessor_poll(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_pkts,
+                         cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats);
+/* The calling thread's context created by coprocessor_setup (or NULL). */
+cop_ctx *coprocessor_ctx(void);
+
+/* ------------------------------------------------------------------------ */
+/* Deterministic synthetic workload (SURVEY.md §8d generator)               */
+/* ------------------------------------------------------------------------ */
+
+#define COP_GEN_FW     0  /* 1k-style firewall rule mix */
+#define COP_GEN_ROUTES 1  /* BGP-like route prefix mix  */
+
+/* Rules: splitmix64(seed). FW: 60% /24, 20% /16-23, 10% /8-15, 10% /25-32
+ * confined to n_long_parents /24s; action 0 w.p. 0.5 else 1..255.
+ * Routes: 55% /24, 25% /17-23, 10% /8-16, 10% /25-32; nh 1..2^24-1. */
+int cop_gen_rules(uint64_t seed, uint32_t n, int kind, uint32_t n_long_parents,
+                  cop_prefix *out);
+
+typedef struct cop_trace_opts {
+    uint32_t n_ports;         /* vports 192.167.10.1..n (default 5) */
+    uint32_t pct_non_ipv4;    /* EtherType 0x86DD percentage (default 2) */
+    uint32_t pct_bad_version; /* IPv4 EtherType, version != 4 (default 0) */
+    uint32_t pct_unknown_dst; /* dst low16 in 0..4 (default 5) */
+    uint32_t pct_vport_dst;   /* dst 192.167.10.x (default 60) */
+    uint32_t pct_src_in_rule; /* src inside a FW rule prefix (default 50) */
+} cop_trace_opts;
+void cop_trace_opts_default(cop_trace_opts *o);
+
+/* n 64-byte frames written at out + i*stride (stride >= 64). */
+int cop_gen_trace(uint64_t seed, uint32_t n, const cop_trace_opts *opts,
+                  const cop_prefix *fw, uint32_t n_fw,
+                  const cop_prefix *routes, uint32_t n_routes,
+                  uint8_t *out, uint32_t stride);
+/* Simple IMIX 64/594/1518 at 7:4:1 packed into a slab at 64-byte aligned
+ * offsets. Call with slab == NULL to get the slab size in *slab_bytes. */
+int cop_gen_imix(uint64_t seed, uint32_t n, const cop_trace_opts *opts,
+                 const cop_prefix *fw, uint32_t n_fw,
+                 const cop_prefix *routes, uint32_t n_routes,
+                 uint8_t *slab, uint64_t *slab_bytes, uint32_t *offsets);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COP_GPU_H */

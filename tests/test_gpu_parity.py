@@ -1,0 +1,232 @@
+"""GPU parity: the HIP pipeline (through the C ABI) against the oracle.
+
+Bit-exact on every field of every per-packet record (verdict, flags, port,
+route next hop) and on the ordered forward list, on seeded synthetic traces
+(SURVEY.md §8d generator). At BASELINE sizes (64k/256k batches) the same
+comparison runs in full — the oracle is C and finishes in well under a
+second — plus size-independent properties of the forward list.
+"""
+import numpy as np
+import pytest
+
+import copgpu as cg
+import oracle as orc
+from helpers import assert_parity, gpu_run, oracle_tables
+
+pytestmark = pytest.mark.gpu
+
+S = cg.STAGE_PARSE
+F = cg.STAGE_FW
+L = cg.STAGE_LPM
+
+
+def fw1k(seed=0x5EED1002):
+    return cg.gen_rules(seed, 1000, cg.GEN_FW, 20)
+
+
+def routes100k(seed=0x5EED2003, n=100000):
+    return cg.gen_rules(seed, n, cg.GEN_ROUTES, 0)
+
+
+def setup_ctx(factory, fw_rules=None, routes=None, stages=S | F, flags=0, fw_cfg=(1024, 24, True),
+              rt_cfg=(1 << 20, 1 << 16, False), **kw):
+    ctx = factory(stages=stages, flags=flags, **kw)
+    if fw_rules is not None:
+        ctx.set_fw_table(cg.LpmTable(fw_rules, *fw_cfg))
+    if routes is not None:
+        ctx.set_route_lpm(cg.LpmTable(routes, *rt_cfg))
+    return ctx
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 255, 256, 257, 1000, 4096, 65536])
+def test_fw_ivt_sizes(gpu_ctx_factory, n):
+    rules = fw1k()
+    ctx = setup_ctx(gpu_ctx_factory, rules)
+    pk = cg.gen_trace(0x5EED0002 + n, n, rules)
+    fwo, rto = oracle_tables(rules)
+    ro, fo, co = orc.process(pk, n, stages=S | F, fw=fwo)
+    ctx.counters(reset=True)
+    rg, fg, _ = gpu_run(ctx, pk, n)
+    assert_parity(rg, fg, ro, fo)
+    cgc = ctx.counters()
+    for k in co:
+        assert cgc[k] == co[k], (k, cgc[k], co[k])
+
+
+def test_fw_dir24_forced(gpu_ctx_factory):
+    rules = fw1k()
+    ctx = setup_ctx(gpu_ctx_factory, rules, flags=cg.CFG_FW_FORCE_DIR24)
+    n = 65536
+    pk = cg.gen_trace(0x5EED0002, n, rules)
+    fwo, _ = oracle_tables(rules)
+    ro, fo, _ = orc.process(pk, n, stages=S | F, fw=fwo)
+    rg, fg, _ = gpu_run(ctx, pk, n)
+    assert_parity(rg, fg, ro, fo)
+
+
+def test_fw_lpm_100k(gpu_ctx_factory):
+    rules = fw1k()
+    routes = routes100k()
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L)
+    n = 65536
+    pk = cg.gen_trace(0x5EED0003, n, rules, routes)
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(pk, n, stages=S | F | L, fw=fwo, route=rto)
+    rg, fg, _ = gpu_run(ctx, pk, n)
+    assert_parity(rg, fg, ro, fo)
+    assert (rg["flags"] & cg.FLAG_ROUTE_HIT).sum() > n // 10   # the route stage really hits
+
+
+def test_imix_fw_lpm(gpu_ctx_factory):
+    rules = fw1k()
+    routes = routes100k()
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L)
+    n = 65536
+    slab, offs = cg.gen_imix(0x5EED0003, n, rules, routes)
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(slab, n, offsets=offs, stages=S | F | L, fw=fwo, route=rto)
+    rg, fg, _ = gpu_run(ctx, slab, n, offsets=offs)
+    assert_parity(rg, fg, ro, fo)
+
+
+@pytest.mark.parametrize("nb", [2, 7, 32])
+def test_multi_batch_submit(gpu_ctx_factory, nb):
+    rules = fw1k()
+    ctx = setup_ctx(gpu_ctx_factory, rules)
+    n = 65536 + 333
+    pk = cg.gen_trace(0x5EED0042, n, rules)
+    fwo, _ = oracle_tables(rules)
+    ro, fo, _ = orc.process(pk, n, stages=S | F, fw=fwo)
+    rg, fg, _ = gpu_run(ctx, pk, n, batches=nb)
+    assert_parity(rg, fg, ro, fo)
+
+
+def test_big_batch_256k_properties(gpu_ctx_factory):
+    rules = fw1k()
+    routes = routes100k()
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L)
+    n = 262144
+    pk = cg.gen_trace(0x5EED0005, n, rules, routes)
+    rg, fg, counts = gpu_run(ctx, pk, n)
+    fwd_mask = rg["verdict"] == cg.FORWARD
+    assert counts[0] == fwd_mask.sum()
+    assert np.all(np.diff(fg.astype(np.int64)) > 0)          # strictly increasing = arrival order
+    assert np.array_equal(fg, np.nonzero(fwd_mask)[0])        # exactly the FORWARD packets
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(pk, n, stages=S | F | L, fw=fwo, route=rto)
+    assert_parity(rg, fg, ro, fo)
+
+
+def test_edge_versions_and_ports(gpu_ctx_factory):
+    """version != 4 (reference UB, defined DROP_NOT_IPV4), non-IPv4
+    EtherType, unknown dst, custom routing table with ports >= n_ports."""
+    rules = fw1k()
+    rt = cg.route_table_default(5)
+    rt[0x1234] = 7           # port beyond nb_active_kni -> DROP_NO_PORT
+    rt[0x2000:0x2100] = 3    # a uniform leaf block
+    ctx = setup_ctx(gpu_ctx_factory, rules, routing_table=rt)
+    n = 20000
+    opts = cg.trace_opts(pct_bad_version=10, pct_non_ipv4=10, pct_unknown_dst=10)
+    pk = cg.gen_trace(0x5EED0077, n, rules, opts=opts)
+    # force some dsts onto the custom entries
+    for i in range(0, n, 97):
+        pk[i * 64 + 32] = 0x12
+        pk[i * 64 + 33] = 0x34
+    fwo, _ = oracle_tables(rules)
+    ro, fo, _ = orc.process(pk, n, rt=rt, stages=S | F, fw=fwo)
+    rg, fg, _ = gpu_run(ctx, pk, n)
+    assert_parity(rg, fg, ro, fo)
+    v = rg["verdict"]
+    for verdict in (cg.FORWARD, cg.DROP_FW, cg.DROP_PARSE, cg.DROP_NOT_IPV4, cg.DROP_NO_PORT):
+        assert (v == verdict).sum() > 0, verdict
+
+
+@pytest.mark.parametrize("stages", [S, S | F, S | L, F, F | L, S | F | L])
+def test_stage_masks(gpu_ctx_factory, stages):
+    rules = fw1k()
+    routes = routes100k(n=20000)
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=stages)
+    n = 30000
+    pk = cg.gen_trace(0x5EED0100 + stages, n, rules, routes)
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(pk, n, stages=stages, fw=fwo, route=rto)
+    rg, fg, _ = gpu_run(ctx, pk, n)
+    assert_parity(rg, fg, ro, fo)
+
+
+def test_reference_rules_json_all_forward(gpu_ctx_factory, tmp_path):
+    """The reference's only fixture (engine/nfs/firewall/rules.json, copied
+    as data under tests/golden/): both rules accept, so every IPv4 packet
+    that reaches the coprocessor is forwarded."""
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "reference_rules.json")
+    ctx = gpu_ctx_factory(stages=S | F)
+    rep = ctx.load_fw_rules_file(path)
+    assert rep.n_added == 2 and rep.n_failed == 0
+    n = 50000
+    pk = cg.gen_trace(0x5EED0001, n)
+    rg, fg, _ = gpu_run(ctx, pk, n)
+    reached = (rg["verdict"] != cg.DROP_PARSE) & (rg["verdict"] != cg.DROP_NO_PORT)
+    assert np.all(rg["verdict"][reached] == cg.FORWARD)
+
+
+def test_empty_batch_and_tiny(gpu_ctx_factory):
+    rules = fw1k()
+    ctx = setup_ctx(gpu_ctx_factory, rules)
+    d = ctx.alloc(64)
+    r = ctx.alloc(64)
+    c = ctx.alloc(16)
+    f = ctx.alloc(64)
+    c.fill(0xFF)
+    ctx.submit([cg.make_batch(d, 0, r, fwd_idx=f, fwd_count=c)])
+    ctx.sync()
+    assert c.download(np.uint32, 1)[0] == 0
+
+
+def test_process_host_end_to_end(gpu_ctx_factory):
+    rules = fw1k()
+    routes = routes100k(n=20000)
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L)
+    n = 10000
+    pk = cg.gen_trace(0x5EED0200, n, rules, routes)
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(pk, n, stages=S | F | L, fw=fwo, route=rto)
+    rg, fg = ctx.process_host(pk, n)
+    assert_parity(rg, fg, ro, fo)
+
+
+def test_tbl8_exhaustion_stop_at_first_error(gpu_ctx_factory):
+    """lpm_setup truncates at the first failed rte_lpm_add: with 30 distinct
+    /24 parents of /25+ rules and number_tbl8s=24 the 25th fails."""
+    ip, depth, nh = [], [], []
+    for k in range(30):
+        ip.append((10 << 24) | (k << 8) | 0x80)
+        depth.append(25)
+        nh.append(1 + k)
+    ip.append(0x0B000000)
+    depth.append(8)
+    nh.append(9)
+    rules = cg.prefixes(ip, depth, nh)
+    t = cg.LpmTable(rules, 1024, 24, True)
+    assert t.report.n_failed == 1 and t.report.first_error_idx == 24 and t.report.n_skipped == 6
+    ctx = setup_ctx(gpu_ctx_factory, rules)
+    n = 4096
+    pk = cg.gen_trace(0x5EED0300, n, rules)
+    fwo, _ = oracle_tables(rules)
+    ro, fo, _ = orc.process(pk, n, stages=S | F, fw=fwo)
+    rg, fg, _ = gpu_run(ctx, pk, n)
+    assert_parity(rg, fg, ro, fo)
+
+
+def test_repeated_submits_epochs(gpu_ctx_factory):
+    """Many launches on one context: ticket base and look-back epochs carry
+    across launches without a reset."""
+    rules = fw1k()
+    ctx = setup_ctx(gpu_ctx_factory, rules)
+    n = 8192
+    pk = cg.gen_trace(0x5EED0400, n, rules)
+    fwo, _ = oracle_tables(rules)
+    ro, fo, _ = orc.process(pk, n, stages=S | F, fw=fwo)
+    for _ in range(50):
+        rg, fg, _ = gpu_run(ctx, pk, n, batches=3)
+    assert_parity(rg, fg, ro, fo)
