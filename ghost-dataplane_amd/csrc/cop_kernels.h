@@ -8,6 +8,10 @@
 
 #define COPK_BLOCK 256
 #define COPK_MAXB 32
+#define COPK_COUNTER_SHARDS 64   /* 16 u64 per shard (128 B) */
+static_assert(sizeof(void *) == 8, "64-bit only");
+#define COPK_LDS_MISC_WORDS 80
+#define COPK_STAMP_WG 65536
 
 #define COPK_TBL_OFF 0
 #define COPK_TBL_IVT 1  /* flattened intervals, binary search in LDS */
@@ -32,19 +36,22 @@ struct CopKBatch {
     uint32_t n;
     uint32_t stride;
     uint32_t data_off;
-    uint32_t tile_begin;      // first launch-relative tile of this batch
     uint32_t ntiles;
-    uint32_t _pad;
 };
 
 struct CopKParams {
     CopKBatch b[COPK_MAXB];
+    uint32_t tile_begin[COPK_MAXB];          // first blockIdx of each batch
+    uint32_t look_begin[COPK_MAXB];          // look-back word offset of each batch
+    unsigned long long ticket_base[COPK_MAXB];
     uint32_t nb;
     uint32_t ntiles;
+    uint32_t uniform_ntiles;  // tiles per batch when all batches are equal, else 0
     uint32_t stages;
     uint32_t n_ports;
     uint32_t compact;
     uint32_t epoch;
+    uint32_t dbg;             // timing-only ablations ($COP_DBG), 0 in production
     // vport routing table (two-level image)
     const uint32_t *rt_top;   // 256 entries: value, or 0x80000000|leaf
     const uint16_t *rt_leaf;  // nleaf * 256
@@ -60,11 +67,11 @@ struct CopKParams {
     // LDS carve (u32 words)
     uint32_t lds_fw_off, lds_lpm_off, lds_misc_off;
     // ordering / accounting state
-    unsigned long long *ticket;
-    unsigned long long ticket_base;
+    unsigned long long *tickets;   // COPK_MAXB counters, one 128-byte line each
     unsigned long long *look;
     unsigned long long *counters;
     uint32_t *err;
+    unsigned long long *stamps;   // diagnostic phase stamps (dbg bit 8)
 };
 
 #ifdef __cplusplus

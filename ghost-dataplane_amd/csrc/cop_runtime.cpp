@@ -40,6 +40,9 @@ struct cop_ctx {
     hipStream_t stream = nullptr;
     cop_config cfg{};
     int ncu = 256;
+    int ppt_override = 0;      // $COP_PPT (1, 4, 8) for experiments; 0 = auto
+    uint32_t dbg = 0;          // $COP_DBG: timing-only kernel ablations
+    unsigned long long *stamps = nullptr;   // dbg bit 8: per-workgroup phase stamps
     char err[256] = {0};
 
     uint32_t *rt_top = nullptr;
@@ -47,8 +50,8 @@ struct cop_ctx {
     uint32_t rt_nleaf = 0;
     DevLpm fw, lpm;
 
-    unsigned long long *ticket = nullptr;
-    unsigned long long ticket_base = 0;
+    unsigned long long *tickets = nullptr;     // COPK_MAXB x 16 u64
+    unsigned long long tbase[COPK_MAXB] = {0};
     unsigned long long *look = nullptr;
     uint32_t look_cap = 0;
     uint32_t epoch = 0;
@@ -140,7 +143,8 @@ void cop_destroy(cop_ctx *c)
     free_lpm(c->lpm);
     if (c->rt_top) (void)hipFree(c->rt_top);
     if (c->rt_leaf) (void)hipFree(c->rt_leaf);
-    if (c->ticket) (void)hipFree(c->ticket);
+    if (c->tickets) (void)hipFree(c->tickets);
+    if (c->stamps) (void)hipFree(c->stamps);
     if (c->look) (void)hipFree(c->look);
     if (c->counters) (void)hipFree(c->counters);
     if (c->h_err) (void)hipHostFree(c->h_err);
@@ -162,8 +166,8 @@ void cop_destroy(cop_ctx *c)
 static int upload_empty_ivt(cop_ctx *c, DevLpm &t)
 {
     const uint32_t zero4[4] = {0, 0, 0, 0};
-    // m = 4 so the LDS copy works in uint4 units; starts[1..3] = 0xFFFFFFFF
-    // would break the search, so repeat starts 0 with value 0 (same function)
+    // empty table: m = 4 (the LDS copy works in uint4 units), every value 0
+    // (miss), so whatever interval the search lands in reads nh 0, no hit
     free_lpm(t);
     HIPCHK(c, hipMalloc(&t.starts, 16));
     HIPCHK(c, hipMalloc(&t.vals, 16));
@@ -238,15 +242,21 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     hipDeviceProp_t prop;
     CREATE_CHK(hipGetDeviceProperties(&prop, c->device));
     c->ncu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (const char *e = getenv("COP_PPT")) {
+        int v = atoi(e);
+        c->ppt_override = (v == 1 || v == 4 || v == 8) ? v : 0;
+    }
+    if (const char *e = getenv("COP_DBG")) c->dbg = (uint32_t)strtoul(e, nullptr, 0);
     CREATE_CHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    CREATE_CHK(hipMalloc(&c->ticket, sizeof(unsigned long long)));
-    CREATE_CHK(hipMemset(c->ticket, 0, sizeof(unsigned long long)));
+    if (c->dbg & 8u) CREATE_CHK(hipMalloc(&c->stamps, (size_t)COPK_STAMP_WG * 8 * 8));
+    CREATE_CHK(hipMalloc(&c->tickets, COPK_MAXB * 16 * sizeof(unsigned long long)));
+    CREATE_CHK(hipMemset(c->tickets, 0, COPK_MAXB * 16 * sizeof(unsigned long long)));
     uint32_t tiles_per_batch = (cfg.max_batch + LOOK_TILE_MIN - 1) / LOOK_TILE_MIN;
     c->look_cap = tiles_per_batch * cfg.max_batches;
     CREATE_CHK(hipMalloc(&c->look, (size_t)c->look_cap * 8));
     CREATE_CHK(hipMemset(c->look, 0, (size_t)c->look_cap * 8));
-    CREATE_CHK(hipMalloc(&c->counters, COP_N_COUNTERS * 8));
-    CREATE_CHK(hipMemset(c->counters, 0, COP_N_COUNTERS * 8));
+    CREATE_CHK(hipMalloc(&c->counters, COPK_COUNTER_SHARDS * COP_N_COUNTERS * 8));
+    CREATE_CHK(hipMemset(c->counters, 0, COPK_COUNTER_SHARDS * COP_N_COUNTERS * 8));
     CREATE_CHK(hipHostMalloc(&c->h_err, 64, hipHostMallocMapped));
     c->h_err[0] = 0;
     CREATE_CHK(hipHostGetDevicePointer((void **)&c->d_err, c->h_err, 0));
@@ -293,22 +303,33 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
     uint32_t m = cop_lpm_merged_intervals(tab, &s, &v);
     if (!s) return set_err(c, -ENOMEM, "interval export failed");
     if (want_ivt && m <= IVT_MAX) {
+        // Eytzinger image: tree[1..M-1] = sorted starts s[1..M-1] in BFS
+        // order (s padded with 0xFFFFFFFF, which only ip 0xFFFFFFFF reaches:
+        // its value, the last real interval's, is repeated in the pads);
+        // vals stay in sorted order, indexed by the search result.
         uint32_t M = next_pow2(m < 4 ? 4 : m);
-        std::vector<uint32_t> hs(M), hv(M);
+        std::vector<uint32_t> sorted(M), tree(M, 0), hv(M);
         for (uint32_t k = 0; k < M; k++) {
-            if (k < m) {
-                hs[k] = s[k];
-                hv[k] = v[k];
-            } else {
-                hs[k] = 0xFFFFFFFFu;
-                hv[k] = v[m - 1];
-            }
+            sorted[k] = k < m ? s[k] : 0xFFFFFFFFu;
+            hv[k] = k < m ? v[k] : v[m - 1];
         }
-        // entries past the real ones must never win: start 0xFFFFFFFF only
-        // matches ip 0xFFFFFFFF, whose value equals the last real interval
+        uint32_t next = 1;
+        // iterative in-order walk of the complete tree on nodes 1..M-1
+        std::vector<uint32_t> stack;
+        uint32_t node = 1;
+        while (node < M || !stack.empty()) {
+            while (node < M) {
+                stack.push_back(node);
+                node *= 2;
+            }
+            node = stack.back();
+            stack.pop_back();
+            tree[node] = sorted[next++];
+            node = 2 * node + 1;
+        }
         HIPCHK(c, hipMalloc(&t.starts, M * 4));
         HIPCHK(c, hipMalloc(&t.vals, M * 4));
-        HIPCHK(c, hipMemcpy(t.starts, hs.data(), M * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(t.starts, tree.data(), M * 4, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(t.vals, hv.data(), M * 4, hipMemcpyHostToDevice));
         t.m = M;
     }
@@ -405,8 +426,12 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
         if (b.fwd_idx || b.fwd_count) compact = true;
     }
     if (c->cfg.flags & COP_CFG_NO_COMPACT) compact = false;
-    // tile size: 1024 packets when there is enough work for >= 2 tiles per CU
-    const int ppt = (total >= (uint64_t)COPK_BLOCK * 4 * 2 * c->ncu) ? 4 : 1;
+    // tile size: the largest of 256 * {8, 4, 1} packets that still gives
+    // at least one tile per CU (fewer tiles = fewer ticket / look-back steps)
+    int ppt = 1;
+    if (total >= (uint64_t)COPK_BLOCK * 8 * c->ncu) ppt = 8;
+    else if (total >= (uint64_t)COPK_BLOCK * 4 * c->ncu) ppt = 4;
+    if (c->ppt_override) ppt = c->ppt_override;
     const uint32_t tile = COPK_BLOCK * ppt;
     uint32_t ntiles = 0;
     for (uint32_t i = 0; i < nb; i++) {
@@ -420,13 +445,18 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
         d.n = b.n;
         d.stride = b.stride;
         d.data_off = b.data_off;
-        d.tile_begin = ntiles;
         d.ntiles = b.n ? (b.n + tile - 1) / tile : 1;   // an empty batch still reports count 0
+        p.tile_begin[i] = ntiles;
+        p.look_begin[i] = ntiles;
+        p.ticket_base[i] = c->tbase[i];
         ntiles += d.ntiles;
     }
     if (ntiles > c->look_cap) return set_err(c, -EINVAL, "too many tiles");
     p.nb = nb;
     p.ntiles = ntiles;
+    p.uniform_ntiles = p.b[0].ntiles;
+    for (uint32_t i = 1; i < nb; i++)
+        if (p.b[i].ntiles != p.b[0].ntiles) p.uniform_ntiles = 0;
     p.stages = stages;
     p.n_ports = c->cfg.n_ports;
     p.compact = compact ? 1u : 0u;
@@ -435,6 +465,7 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
         c->epoch = 1;
     }
     p.epoch = c->epoch;
+    p.dbg = c->dbg;
     p.rt_top = c->rt_top;
     p.rt_leaf = c->rt_leaf;
     p.rt_nleaf = c->rt_nleaf;
@@ -455,21 +486,18 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
     p.lds_lpm_off = off;
     off += 2 * p.lpm_m;
     p.lds_misc_off = off;
-    off += 4 * 4 + 8;
+    off += COPK_LDS_MISC_WORDS;
     const uint32_t lds_bytes = off * 4;
     if (lds_bytes > 160 * 1024) return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_bytes);
-    p.ticket = c->ticket;
-    p.ticket_base = c->ticket_base;
+    p.tickets = c->tickets;
     p.look = c->look;
     p.counters = c->counters;
     p.err = c->d_err;
-
-    uint32_t per_cu = (160u * 1024u) / (lds_bytes < 1024 ? 1024 : lds_bytes);
-    if (per_cu > 8) per_cu = 8;
-    if (per_cu < 1) per_cu = 1;
-    uint32_t grid = (uint32_t)c->ncu * per_cu;
-    if (grid > ntiles) grid = ntiles;
-    c->ticket_base += (unsigned long long)ntiles + grid;
+    p.stamps = c->stamps;
+    if ((c->dbg & 8u) && ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
+    const uint32_t grid = ntiles;   // one tile per workgroup
+    if (compact && !(c->dbg & 2u))
+        for (uint32_t i = 0; i < nb; i++) c->tbase[i] += p.b[i].ntiles;
 
     HIPCHK(c, hipSetDevice(c->device));
     if (c->timing) {
@@ -478,7 +506,8 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
     }
     hipError_t e = copk_launch(&p, fw_mode, lpm_mode, imix ? 1 : 0, ppt, grid, lds_bytes, c->stream);
     if (e != hipSuccess) {
-        c->ticket_base -= (unsigned long long)ntiles + grid;
+        if (compact && !(c->dbg & 2u))
+            for (uint32_t i = 0; i < nb; i++) c->tbase[i] -= p.b[i].ntiles;
         return set_err(c, -EIO, "launch: %s", hipGetErrorString(e));
     }
     if (c->timing) {
@@ -570,8 +599,13 @@ int cop_counters_read(cop_ctx *c, cop_counters *out, int reset)
     if (!c || !out) return -EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipMemcpy(out, c->counters, sizeof(cop_counters), hipMemcpyDeviceToHost));
-    if (reset) HIPCHK(c, hipMemset(c->counters, 0, sizeof(cop_counters)));
+    std::vector<uint64_t> sh((size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS);
+    HIPCHK(c, hipMemcpy(sh.data(), c->counters, sh.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t sum[COP_N_COUNTERS] = {0};
+    for (int s = 0; s < COPK_COUNTER_SHARDS; s++)
+        for (int k = 0; k < COP_N_COUNTERS; k++) sum[k] += sh[(size_t)s * COP_N_COUNTERS + k];
+    memcpy(out, sum, sizeof(cop_counters));
+    if (reset) HIPCHK(c, hipMemset(c->counters, 0, sh.size() * 8));
     return 0;
 }
 
@@ -660,6 +694,17 @@ int cop_timer_stop(cop_ctx *c, double *ms)
     HIPCHK(c, hipEventElapsedTime(&f, c->t0, c->t1));
     *ms = f;
     return 0;
+}
+
+/* diagnostic (not in the public header): copy the phase stamps of the last
+ * launch made with $COP_DBG bit 8; returns the number of u64 copied */
+int cop_debug_stamps(cop_ctx *c, uint64_t *out, uint32_t max_words)
+{
+    if (!c || !c->stamps) return -EINVAL;
+    uint32_t n = max_words < COPK_STAMP_WG * 8 ? max_words : COPK_STAMP_WG * 8;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, c->stamps, (size_t)n * 8, hipMemcpyDeviceToHost));
+    return (int)n;
 }
 
 int cop_launch_timing(cop_ctx *c, int enable)

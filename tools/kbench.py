@@ -31,10 +31,17 @@ def main():
     P = 100
     ctxs = {}
 
-    def ctx_for(stages, flags):
-        key = (stages, flags)
+    def ctx_for(stages, flags, env=()):
+        key = (stages, flags, env)
         if key not in ctxs:
+            saved = {k: os.environ.get(k) for k, _ in env}
+            os.environ.update(dict(env))
             c = cg.Context(stages=stages, flags=flags, max_batch=262144)
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
             c.set_fw_table(cg.LpmTable(fw_rules, 1024, 24))
             c.set_route_lpm(cg.LpmTable(routes, 1 << 20, 1 << 16, False))
             ctxs[key] = c
@@ -59,12 +66,18 @@ def main():
         "p_only_L16": (S, 0, 16, True),
         "fw_lpm_L16": (S | F | L, 0, 16, True),
     }
+    for ppt in (1, 4, 8):
+        variants[f"fw_L16_p{ppt}"] = (S | F, 0, 16, True, (("COP_PPT", str(ppt)),))
+    # timing-only ablations (COP_DBG bits: 1 no counter atomics, 2 static tiles, 4 no LDS staging)
+    for dbg in (1, 2, 3, 7):
+        variants[f"nc_dbg{dbg}"] = (S | F, 0, 16, False, (("COP_DBG", str(dbg)),))
+    variants["c_dbg1"] = (S | F, 0, 16, True, (("COP_DBG", "1"),))
     names = [v for v in args.variants.split(",") if v] or list(variants)
     res = {n: [] for n in names}
     for r in range(args.rounds):
         for n in names:
-            stages, flags, Lb, compact = variants[n]
-            ctx = ctx_for(stages, flags)
+            stages, flags, Lb, compact, *env = variants[n]
+            ctx = ctx_for(stages, flags, env[0] if env else ())
             def sub(i0):
                 bl = []
                 for j in range(Lb):
@@ -89,7 +102,7 @@ def main():
             res[n].append((ms, wall / args.launches))
     print(f"{'variant':22s} {'kern_us':>9s} {'GB/s':>8s} {'frac':>6s} {'Mpkt/s(stream)':>15s}")
     for n in names:
-        stages, flags, Lb, compact = variants[n]
+        stages, flags, Lb, compact, *_ = variants[n]
         k = np.median([a for a, _ in res[n]])
         w = np.median([b for _, b in res[n]])
         gbs = 72 * B * Lb / (k * 1e-3) / 1e9

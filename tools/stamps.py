@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-workgroup phase timeline of one launch (COP_DBG bit 8,
+s_memrealtime at 100 MHz). Reports, over workgroups, the median / p90 of
+each phase and the launch span. Timing-only build flag; outputs of that
+launch are still checked by nothing here.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ghost-dataplane_amd"))
+os.environ["COP_DBG"] = str(8 | int(os.environ.get("EXTRA_DBG", "0")))
+import copgpu as cg  # noqa: E402
+
+S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
+PH = ["ticket+stage", "loads+P", "lookups", "store", "compact", "tail"]
+
+
+def run(stages, Lb, compact, label):
+    fw = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
+    routes = cg.gen_rules(0x5EED2004, 100000, cg.GEN_ROUTES, 0)
+    ctx = cg.Context(stages=stages)
+    ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
+    ctx.set_route_lpm(cg.LpmTable(routes, 1 << 20, 1 << 16, False))
+    B = 65536
+    P = 64
+    dp = ctx.alloc(P * B * 64)
+    for i in range(0, P, 16):
+        dp.upload(cg.gen_trace(0x5EED0002 + i, 16 * B, fw, routes), i * B * 64)
+    dr = ctx.alloc(P * B * 8)
+    df = ctx.alloc(P * B * 4)
+    dc = ctx.alloc(P * 4)
+    for it in range(6):
+        bl = []
+        for j in range(Lb):
+            i = (it * Lb + j) % P
+            bl.append(cg.make_batch(dp.addr + i * B * 64, B, dr.addr + i * B * 8,
+                                    fwd_idx=(df.addr + i * B * 4) if compact else None,
+                                    fwd_count=(dc.addr + i * 4) if compact else None))
+        ctx.submit(bl)
+    ctx.sync()
+    lib = cg.lib()
+    lib.cop_debug_stamps.restype = ctypes.c_int
+    lib.cop_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+    n = 65536 * 8
+    buf = np.zeros(n, dtype=np.uint64)
+    k = lib.cop_debug_stamps(ctx.handle, buf.ctypes.data_as(ctypes.c_void_p), n)
+    st = buf[:k].reshape(-1, 8).astype(np.int64)
+    st = st[st[:, 0] > 0]
+    t0 = st[:, 0].min()
+    span = (st[:, 6].max() - t0) * 10 / 1000
+    print(f"== {label}: {len(st)} workgroups, span {span:.2f} us")
+    starts = (st[:, 0] - t0) * 10 / 1000
+    print(f"   start spread  median {np.median(starts):.2f}  p90 {np.percentile(starts, 90):.2f}  max {starts.max():.2f} us")
+    ends = (st[:, 6] - t0) * 10 / 1000
+    print(f"   end           min {ends.min():.2f}  median {np.median(ends):.2f}  max {ends.max():.2f} us")
+    for a, name in enumerate(PH):
+        b = a + 1
+        if not compact and a == 4:
+            d = (st[:, 6] - st[:, 4]) * 10 / 1000
+            print(f"   {'store->end':14s} median {np.median(d):6.2f}  p90 {np.percentile(d, 90):6.2f} us")
+            break
+        d = (st[:, b] - st[:, a]) * 10 / 1000
+        print(f"   {name:14s} median {np.median(d):6.2f}  p90 {np.percentile(d, 90):6.2f} us")
+    ctx.close()
+
+
+if __name__ == "__main__":
+    run(S | F, 16, True, "fw L16 compact")
+    run(S | F, 16, False, "fw L16 no-compact")
+    run(S | F, 1, True, "fw L1 compact")
+    run(S | F | L, 16, True, "fw+lpm L16 compact")
