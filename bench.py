@@ -29,6 +29,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ghost-dataplane_amd"))
 
+import copdist  # noqa: E402
 import copgpu as cg  # noqa: E402
 
 METRIC = "Mpkt/s device-resident coprocessor NF pipeline (64B pkts); HBM GB/s vs peak"
@@ -55,8 +56,8 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=480)
-    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=6400)
+    ap.add_argument("--warmup", type=int, default=640)
     ap.add_argument("--workload", default="fw1k", choices=sorted(WORKLOADS))
     ap.add_argument("--per-launch", type=int, default=16, help="batches per kernel launch")
     ap.add_argument("--pool-mib", type=int, default=400, help="distinct input bytes per GPU")
@@ -64,25 +65,14 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = copdist.env()
     W = WORKLOADS[args.workload]
     B = W["batch"]
     Lb = max(1, min(args.per_launch, 32))
 
-    lib = cg.lib()   # load the HIP runtime the product links (before torch)
-    ndev = cg.device_count()
-    if ndev < 1:
-        raise SystemExit("bench: no GPU visible")
-    dev = local % ndev
-
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        tdist.init_process_group("gloo", rank=rank, world_size=world)
-        dist = (torch, tdist)
+    cg.lib()   # load the HIP runtime the product links (before torch)
+    dev = copdist.device_for(local, cg.device_count())
+    group = copdist.Group(rank, world, "gloo")
 
     # ---- tables (identical on every rank; packets differ per rank) ----
     cid = W["cid"]
@@ -103,7 +93,7 @@ def main():
     pool_bytes = args.pool_mib << 20
     t0 = time.time()
     if W["imix"]:
-        slab, offs = cg.gen_imix(0x5EED0000 + cid + 1000 * rank, B, fw_rules, routes)
+        slab, offs = cg.gen_imix(copdist.shard_seed(0x5EED0000 + cid, rank), B, fw_rules, routes)
         per_batch = slab.nbytes + offs.nbytes
     else:
         per_batch = B * 64
@@ -121,7 +111,7 @@ def main():
         chunk = 16
         for i in range(0, P, chunk):
             k = min(chunk, P - i)
-            pk = cg.gen_trace(0x5EED0000 + cid + 1000 * rank + i, k * B, fw_rules, routes)
+            pk = cg.gen_trace(copdist.shard_seed(0x5EED0000 + cid, rank, i), k * B, fw_rules, routes)
             d_pkts.upload(pk, i * per_batch)
     log(f"[rank {rank}] pool: {P} batches x {B} pkts ({P * per_batch / 2**20:.0f} MiB) in {time.time() - t0:.1f}s")
 
@@ -141,26 +131,17 @@ def main():
             ctx.submit([batch(s + j) for j in range(k)])
             s += k
 
-    def barrier():
-        if dist:
-            dist[1].barrier()
-
     # ---- warmup, then exactly K timed steps ----
     run_steps(0, args.warmup)
     ctx.sync()
-    barrier()
+    group.barrier()
     ctx.sync()
     t0 = time.perf_counter()
     run_steps(args.warmup, args.steps)
     ctx.sync()
     t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    if dist:
-        torch, tdist = dist
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    group.barrier()
+    elapsed = group.max(t1 - t0)
     total_pkts = world * args.steps * B
     value = total_pkts / elapsed / 1e6
     log(f"[rank {rank}] timed {args.steps} steps in {elapsed * 1e3:.2f} ms -> {value:.1f} Mpkt/s (all ranks)")
@@ -245,8 +226,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
-    if dist:
-        dist[1].destroy_process_group()
+    group.close()
 
 
 if __name__ == "__main__":

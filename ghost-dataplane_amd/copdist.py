@@ -1,0 +1,70 @@
+"""One process per GPU for the coprocessor pipeline.
+
+Packet batches shard with no data-path exchange: every rank owns one GPU,
+one context, its own packet stream and a replica of the tables. The only
+collectives are control-plane ones, over gloo on host tensors:
+  - a barrier around the timed region and the max of elapsed times,
+  - sums of u64 counter arrays (cop_counters, per-rule hits) at a reporting
+    interval — the analogue of the reference's print_stats every
+    PRINT_DELAY = 2 s (switch.h:23, switch.c:33-90).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+
+def env():
+    """(rank, world, local_rank) as set by torch.distributed.run."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def device_for(local_rank: int, ndev: int) -> int:
+    if ndev < 1:
+        raise RuntimeError("no GPU visible")
+    return local_rank % ndev
+
+
+def shard_seed(base: int, rank: int, index: int = 0) -> int:
+    """Seed of rank `rank`'s `index`-th trace chunk: disjoint per rank."""
+    return (base + 1000 * rank + index) & 0xFFFFFFFFFFFFFFFF
+
+
+class Group:
+    """Thin control-plane group; world == 1 needs no torch at all."""
+
+    def __init__(self, rank: int, world: int, backend: str = "gloo"):
+        self.rank, self.world = rank, world
+        self._dist = None
+        if world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                dist.init_process_group(backend, rank=rank, world_size=world)
+            self._dist = dist
+
+    def barrier(self):
+        if self._dist:
+            self._dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self._dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_u64(self, a: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        if not self._dist:
+            return a.copy()
+        import torch
+        t = torch.from_numpy(a.view(np.int64).copy())
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM)
+        return t.numpy().view(np.uint64)
+
+    def close(self):
+        if self._dist and self._dist.is_initialized():
+            self._dist.destroy_process_group()
