@@ -147,13 +147,19 @@ def main():
     log(f"[rank {rank}] timed {args.steps} steps in {elapsed * 1e3:.2f} ms -> {value:.1f} Mpkt/s (all ranks)")
 
     # ---- kernel duration per launch (HIP events on the context stream) ----
+    ctx.counters(reset=True)
     ctx.launch_timing(True)
-    nl = max(8, args.steps // Lb)
+    nl = max(8, min(200, args.steps // Lb))
     run_steps(0, nl * Lb)
     ctx.sync()
     mean_ms, n_launch = ctx.launch_timing_read(reset=True)
     ctx.launch_timing(False)
-    bytes_per_pkt = 76 if W["imix"] else 72   # 64 B header line (+4 B offset) + 8 B record
+    cnt = ctx.counters()
+    fwd_frac = cnt["forward"] / max(1, cnt["rx"])
+    # algorithmic bytes per packet: the 64 B header line (+4 B offset for
+    # IMIX), the 8 B result record, and 4 B per forwarded packet for the
+    # ordered forward list
+    bytes_per_pkt = (76 if W["imix"] else 72) + 4 * fwd_frac
     alg_bytes = bytes_per_pkt * B * Lb
     achieved = alg_bytes / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
 
@@ -197,7 +203,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "algorithmic_bytes_per_pkt": bytes_per_pkt,
+            "algorithmic_bytes_per_pkt": round(bytes_per_pkt, 3),
+            "traffic_per_algorithmic": (round(traffic / alg_bytes, 4) if traffic else None),
             "kernel_ms_per_launch": round(mean_ms, 6),
             "launches_timed": int(n_launch),
         },

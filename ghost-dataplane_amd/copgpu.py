@@ -55,7 +55,7 @@ class LpmReport(Structure):
 class Config(Structure):
     _fields_ = [("device", c_int), ("stages", c_uint32), ("n_ports", c_uint32),
                 ("max_batch", c_uint32), ("max_batches", c_uint32), ("flags", c_uint32),
-                ("routing_table", POINTER(c_uint16))]
+                ("n_streams", c_uint32), ("routing_table", POINTER(c_uint16))]
 
 
 class Batch(Structure):
@@ -99,6 +99,7 @@ SIGNATURES = {
     "cop_sync": (c_int, [c_void_p]),
     "cop_poll": (c_int, [c_void_p]),
     "cop_process_host": (c_int, [c_void_p, POINTER(c_void_p), c_uint32, c_void_p, c_void_p, c_void_p]),
+    "cop_process_host_stream": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
     "cop_counters_read": (c_int, [c_void_p, c_void_p, c_int]),
     "cop_counters_device_ptr": (c_void_p, [c_void_p]),
     "cop_dev_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
@@ -323,11 +324,13 @@ class Context:
     """One GPU context (cop_ctx): device, stream, NF tables."""
 
     def __init__(self, device=0, stages=STAGE_PARSE | STAGE_FW, n_ports=5, max_batch=262144,
-                 max_batches=32, flags=0, routing_table: np.ndarray | None = None):
+                 max_batches=32, flags=0, routing_table: np.ndarray | None = None, n_streams=None):
         cfg = Config()
         lib().cop_config_default(byref(cfg))
         cfg.device, cfg.stages, cfg.n_ports = device, stages, n_ports
         cfg.max_batch, cfg.max_batches, cfg.flags = max_batch, max_batches, flags
+        if n_streams is not None:
+            cfg.n_streams = n_streams
         self._rt = None
         if routing_table is not None:
             self._rt = np.ascontiguousarray(routing_table, dtype=np.uint16)
@@ -401,6 +404,14 @@ class Context:
         _check(lib().cop_process_host(self.handle, ptrs, n, _ptr(res), _ptr(fwd), byref(cnt)), self,
                "process_host")
         return res, fwd[: cnt.value]
+
+    def process_host_stream(self, ptrs: np.ndarray, batch: int) -> np.ndarray:
+        """Streaming end-to-end path over host packet addresses (u64 array)."""
+        ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        res = np.zeros(len(ptrs), dtype=RESULT_DT)
+        _check(lib().cop_process_host_stream(self.handle, _ptr(ptrs), len(ptrs), batch, _ptr(res)), self,
+               "process_host_stream")
+        return res
 
     def timer_start(self):
         _check(lib().cop_timer_start(self.handle), self, "timer_start")

@@ -1,7 +1,9 @@
 // cop_runtime.cpp — GPU context behind the C ABI (include/cop_gpu.h).
 //
-// One context = one HIP device + one in-order stream + the device copies of
-// the NF tables. It replaces the process-global NF state of the reference
+// One context = one HIP device + 1..4 launch lanes (a HIP stream each, with
+// its own ticket counters and look-back words, so launches on different
+// lanes can run concurrently) + the device copies of the NF tables. It
+// replaces the process-global NF state of the reference
 // (lpm_tbl / rules / stats globals, firewall.h:107-110, shared and raced by
 // the five coprocessor threads) with per-context state: one context per
 // coprocessor thread or per GPU, no globals.
@@ -23,7 +25,8 @@ namespace {
 
 constexpr uint32_t IVT_MAX = 8192;          // LDS interval entries per table (64 KiB)
 constexpr uint32_t LOOK_TILE_MIN = COPK_BLOCK;
-constexpr int TIMING_SLOTS = 1024;
+constexpr int TIMING_SLOTS = 256;   // per lane
+constexpr int MAX_LANES = 4;
 
 struct DevLpm {
     bool loaded = false;
@@ -33,11 +36,33 @@ struct DevLpm {
     uint32_t n_ext = 0;
 };
 
+struct Lane {
+    hipStream_t s = nullptr;
+    unsigned long long *tickets = nullptr;          // COPK_MAXB x 16 u64
+    unsigned long long tbase[COPK_MAXB] = {0};
+    unsigned long long *look = nullptr;
+    uint32_t epoch = 0;
+    hipEvent_t ev[TIMING_SLOTS][2];
+    int ev_head = 0, ev_count = 0, ev_created = 0;
+    hipEvent_t join = nullptr;                      // timer joins
+    // streaming host-path slot
+    uint8_t *h_stage = nullptr, *d_stage = nullptr;
+    cop_result *h_res = nullptr, *d_res = nullptr;
+    uint32_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    uint64_t first = 0;
+    uint32_t n = 0;
+};
+
 }  // namespace
 
 struct cop_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // lane 0's stream (helpers, uploads)
+    Lane lane[MAX_LANES];
+    int n_lanes = 1;
+    int next_lane = 0;
     cop_config cfg{};
     int ncu = 256;
     int ppt_override = 0;      // $COP_PPT (1, 4, 8) for experiments; 0 = auto
@@ -50,20 +75,13 @@ struct cop_ctx {
     uint32_t rt_nleaf = 0;
     DevLpm fw, lpm;
 
-    unsigned long long *tickets = nullptr;     // COPK_MAXB x 16 u64
-    unsigned long long tbase[COPK_MAXB] = {0};
-    unsigned long long *look = nullptr;
     uint32_t look_cap = 0;
-    uint32_t epoch = 0;
-    unsigned long long *counters = nullptr;     // owned
-    unsigned long long *counters_ext = nullptr; // caller-provided (unused now)
+    unsigned long long *counters = nullptr;     // COPK_COUNTER_SHARDS x 16 u64
     uint32_t *h_err = nullptr;                  // host-mapped
     uint32_t *d_err = nullptr;
 
     hipEvent_t t0 = nullptr, t1 = nullptr;
     bool timing = false;
-    hipEvent_t ev[TIMING_SLOTS][2];
-    int ev_head = 0, ev_count = 0, ev_created = 0;
     double ev_sum_ms = 0;
     uint64_t ev_n = 0;
 
@@ -113,6 +131,7 @@ void cop_config_default(cop_config *cfg)
     cfg->max_batch = 262144;
     cfg->max_batches = COPK_MAXB;
     cfg->flags = 0;
+    cfg->n_streams = 2;
     cfg->routing_table = nullptr;
 }
 
@@ -138,21 +157,32 @@ void cop_destroy(cop_ctx *c)
 {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (int l = 0; l < MAX_LANES; l++)
+        if (c->lane[l].s) (void)hipStreamSynchronize(c->lane[l].s);
     free_lpm(c->fw);
     free_lpm(c->lpm);
     if (c->rt_top) (void)hipFree(c->rt_top);
     if (c->rt_leaf) (void)hipFree(c->rt_leaf);
-    if (c->tickets) (void)hipFree(c->tickets);
     if (c->stamps) (void)hipFree(c->stamps);
-    if (c->look) (void)hipFree(c->look);
     if (c->counters) (void)hipFree(c->counters);
     if (c->h_err) (void)hipHostFree(c->h_err);
     if (c->t0) (void)hipEventDestroy(c->t0);
     if (c->t1) (void)hipEventDestroy(c->t1);
-    for (int i = 0; i < c->ev_created; i++) {
-        (void)hipEventDestroy(c->ev[i][0]);
-        (void)hipEventDestroy(c->ev[i][1]);
+    for (int l = 0; l < MAX_LANES; l++) {
+        Lane &L = c->lane[l];
+        if (L.tickets) (void)hipFree(L.tickets);
+        if (L.look) (void)hipFree(L.look);
+        for (int i = 0; i < L.ev_created; i++) {
+            (void)hipEventDestroy(L.ev[i][0]);
+            (void)hipEventDestroy(L.ev[i][1]);
+        }
+        if (L.join) (void)hipEventDestroy(L.join);
+        if (L.done) (void)hipEventDestroy(L.done);
+        if (L.h_stage) (void)hipHostFree(L.h_stage);
+        if (L.h_res) (void)hipHostFree(L.h_res);
+        if (L.d_stage) (void)hipFree(L.d_stage);
+        if (L.d_res) (void)hipFree(L.d_res);
+        if (L.s && L.s != c->stream) (void)hipStreamDestroy(L.s);
     }
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->d_stage) (void)hipFree(c->d_stage);
@@ -178,9 +208,13 @@ static int upload_empty_ivt(cop_ctx *c, DevLpm &t)
     return 0;
 }
 
+static int sync_lanes(cop_ctx *c);
+
 int cop_set_routing_table(cop_ctx *c, const uint16_t *rt)
 {
     if (!c || !rt) return -EINVAL;
+    if (c->lane[0].s)
+        if (int rc = sync_lanes(c)) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     uint32_t top[256];
     std::vector<uint16_t> leaves;
@@ -217,8 +251,10 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (cfg_in) cfg = *cfg_in;
     else cop_config_default(&cfg);
     if (cfg.max_batches == 0 || cfg.max_batches > COPK_MAXB || cfg.max_batch == 0 ||
-        cfg.max_batch > (1u << 30) || cfg.n_ports == 0 || cfg.n_ports > 0xFFFFu)
+        cfg.max_batch > (1u << 30) || cfg.n_ports == 0 || cfg.n_ports > 0xFFFFu ||
+        cfg.n_streams > MAX_LANES)
         return -EINVAL;
+    if (cfg.n_streams == 0) cfg.n_streams = 1;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
     if (cfg.device < 0 || cfg.device >= ndev) return -ENODEV;
@@ -247,14 +283,35 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
         c->ppt_override = (v == 1 || v == 4 || v == 8) ? v : 0;
     }
     if (const char *e = getenv("COP_DBG")) c->dbg = (uint32_t)strtoul(e, nullptr, 0);
-    CREATE_CHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (const char *e = getenv("COP_STREAMS")) {
+        int v = atoi(e);
+        if (v >= 1 && v <= MAX_LANES) cfg.n_streams = (uint32_t)v;
+    }
+    c->n_lanes = (int)cfg.n_streams;
+    c->cfg.n_streams = cfg.n_streams;
     if (c->dbg & 8u) CREATE_CHK(hipMalloc(&c->stamps, (size_t)COPK_STAMP_WG * 8 * 8));
-    CREATE_CHK(hipMalloc(&c->tickets, COPK_MAXB * 16 * sizeof(unsigned long long)));
-    CREATE_CHK(hipMemset(c->tickets, 0, COPK_MAXB * 16 * sizeof(unsigned long long)));
     uint32_t tiles_per_batch = (cfg.max_batch + LOOK_TILE_MIN - 1) / LOOK_TILE_MIN;
     c->look_cap = tiles_per_batch * cfg.max_batches;
-    CREATE_CHK(hipMalloc(&c->look, (size_t)c->look_cap * 8));
-    CREATE_CHK(hipMemset(c->look, 0, (size_t)c->look_cap * 8));
+    for (int l = 0; l < c->n_lanes; l++) {
+        Lane &L = c->lane[l];
+        CREATE_CHK(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
+        CREATE_CHK(hipMalloc(&L.tickets, COPK_MAXB * 16 * sizeof(unsigned long long)));
+        CREATE_CHK(hipMemset(L.tickets, 0, COPK_MAXB * 16 * sizeof(unsigned long long)));
+        CREATE_CHK(hipMalloc(&L.look, (size_t)c->look_cap * 8));
+        CREATE_CHK(hipMemset(L.look, 0, (size_t)c->look_cap * 8));
+        CREATE_CHK(hipEventCreateWithFlags(&L.join, hipEventDisableTiming));
+        CREATE_CHK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
+        for (int i = 0; i < TIMING_SLOTS; i++) {
+            CREATE_CHK(hipEventCreate(&L.ev[i][0]));
+            if (hipEventCreate(&L.ev[i][1]) != hipSuccess) {
+                (void)hipEventDestroy(L.ev[i][0]);
+                cop_destroy(c);
+                return -EIO;
+            }
+            L.ev_created = i + 1;
+        }
+    }
+    c->stream = c->lane[0].s;
     CREATE_CHK(hipMalloc(&c->counters, COPK_COUNTER_SHARDS * COP_N_COUNTERS * 8));
     CREATE_CHK(hipMemset(c->counters, 0, COPK_COUNTER_SHARDS * COP_N_COUNTERS * 8));
     CREATE_CHK(hipHostMalloc(&c->h_err, 64, hipHostMallocMapped));
@@ -262,16 +319,6 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     CREATE_CHK(hipHostGetDevicePointer((void **)&c->d_err, c->h_err, 0));
     CREATE_CHK(hipEventCreate(&c->t0));
     CREATE_CHK(hipEventCreate(&c->t1));
-    for (int i = 0; i < TIMING_SLOTS; i++) {
-        CREATE_CHK(hipEventCreate(&c->ev[i][0]));
-        if (hipEventCreate(&c->ev[i][1]) != hipSuccess) {
-            (void)hipEventDestroy(c->ev[i][0]);
-            cop_destroy(c);
-            return -EIO;
-        }
-        c->ev_created = i + 1;
-    }
-    c->ev_count = 0;
 #undef CREATE_CHK
     uint16_t *rt = (uint16_t *)malloc(COP_ROUTING_TBL_SZ * sizeof(uint16_t));
     if (!rt) {
@@ -293,10 +340,16 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     return 0;
 }
 
-static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt)
+static int sync_lanes(cop_ctx *c)
 {
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int l = 0; l < c->n_lanes; l++) HIPCHK(c, hipStreamSynchronize(c->lane[l].s));
+    return 0;
+}
+
+static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt)
+{
+    if (int rc = sync_lanes(c)) return rc;
     free_lpm(t);
     // interval form for LDS
     uint32_t *s = nullptr, *v = nullptr;
@@ -384,22 +437,31 @@ static int pick_mode(const cop_ctx *c, const DevLpm &t, bool enabled, bool force
     return COPK_TBL_IVT;  // empty table (m = 4)
 }
 
-static void harvest_one(cop_ctx *c)
+static void harvest_one(cop_ctx *c, Lane &L)
 {
-    int idx = (c->ev_head - c->ev_count + TIMING_SLOTS) % TIMING_SLOTS;
+    int idx = (L.ev_head - L.ev_count + TIMING_SLOTS) % TIMING_SLOTS;
     float ms = 0;
-    if (hipEventSynchronize(c->ev[idx][1]) == hipSuccess &&
-        hipEventElapsedTime(&ms, c->ev[idx][0], c->ev[idx][1]) == hipSuccess) {
+    if (hipEventSynchronize(L.ev[idx][1]) == hipSuccess &&
+        hipEventElapsedTime(&ms, L.ev[idx][0], L.ev[idx][1]) == hipSuccess) {
         c->ev_sum_ms += ms;
         c->ev_n++;
     }
-    c->ev_count--;
+    L.ev_count--;
 }
+
+static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb);
 
 int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
 {
     if (!c || (!batches && nb)) return -EINVAL;
     if (nb == 0) return 0;
+    Lane &L = c->lane[c->next_lane];
+    c->next_lane = (c->next_lane + 1) % c->n_lanes;
+    return submit_on(c, L, batches, nb);
+}
+
+static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb)
+{
     if (nb > c->cfg.max_batches) return set_err(c, -EINVAL, "nb %u > max_batches", nb);
     const uint32_t stages = c->cfg.stages;
     const bool fw_on = (stages & COP_STAGE_FW) != 0;
@@ -448,7 +510,7 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
         d.ntiles = b.n ? (b.n + tile - 1) / tile : 1;   // an empty batch still reports count 0
         p.tile_begin[i] = ntiles;
         p.look_begin[i] = ntiles;
-        p.ticket_base[i] = c->tbase[i];
+        p.ticket_base[i] = L.tbase[i];
         ntiles += d.ntiles;
     }
     if (ntiles > c->look_cap) return set_err(c, -EINVAL, "too many tiles");
@@ -460,11 +522,11 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
     p.stages = stages;
     p.n_ports = c->cfg.n_ports;
     p.compact = compact ? 1u : 0u;
-    if (++c->epoch == 0) {
-        HIPCHK(c, hipMemsetAsync(c->look, 0, (size_t)c->look_cap * 8, c->stream));
-        c->epoch = 1;
+    if (++L.epoch == 0) {
+        HIPCHK(c, hipMemsetAsync(L.look, 0, (size_t)c->look_cap * 8, L.s));
+        L.epoch = 1;
     }
-    p.epoch = c->epoch;
+    p.epoch = L.epoch;
     p.dbg = c->dbg;
     p.rt_top = c->rt_top;
     p.rt_leaf = c->rt_leaf;
@@ -489,31 +551,31 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
     off += COPK_LDS_MISC_WORDS;
     const uint32_t lds_bytes = off * 4;
     if (lds_bytes > 160 * 1024) return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_bytes);
-    p.tickets = c->tickets;
-    p.look = c->look;
+    p.tickets = L.tickets;
+    p.look = L.look;
     p.counters = c->counters;
     p.err = c->d_err;
     p.stamps = c->stamps;
     if ((c->dbg & 8u) && ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
     const uint32_t grid = ntiles;   // one tile per workgroup
     if (compact && !(c->dbg & 2u))
-        for (uint32_t i = 0; i < nb; i++) c->tbase[i] += p.b[i].ntiles;
+        for (uint32_t i = 0; i < nb; i++) L.tbase[i] += p.b[i].ntiles;
 
     HIPCHK(c, hipSetDevice(c->device));
     if (c->timing) {
-        if (c->ev_count == TIMING_SLOTS) harvest_one(c);
-        HIPCHK(c, hipEventRecord(c->ev[c->ev_head][0], c->stream));
+        if (L.ev_count == TIMING_SLOTS) harvest_one(c, L);
+        HIPCHK(c, hipEventRecord(L.ev[L.ev_head][0], L.s));
     }
-    hipError_t e = copk_launch(&p, fw_mode, lpm_mode, imix ? 1 : 0, ppt, grid, lds_bytes, c->stream);
+    hipError_t e = copk_launch(&p, fw_mode, lpm_mode, imix ? 1 : 0, ppt, grid, lds_bytes, L.s);
     if (e != hipSuccess) {
         if (compact && !(c->dbg & 2u))
-            for (uint32_t i = 0; i < nb; i++) c->tbase[i] -= p.b[i].ntiles;
+            for (uint32_t i = 0; i < nb; i++) L.tbase[i] -= p.b[i].ntiles;
         return set_err(c, -EIO, "launch: %s", hipGetErrorString(e));
     }
     if (c->timing) {
-        HIPCHK(c, hipEventRecord(c->ev[c->ev_head][1], c->stream));
-        c->ev_head = (c->ev_head + 1) % TIMING_SLOTS;
-        c->ev_count++;
+        HIPCHK(c, hipEventRecord(L.ev[L.ev_head][1], L.s));
+        L.ev_head = (L.ev_head + 1) % TIMING_SLOTS;
+        L.ev_count++;
     }
     return 0;
 }
@@ -521,8 +583,7 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
 int cop_sync(cop_ctx *c)
 {
     if (!c) return -EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = sync_lanes(c)) return rc;
     if (c->h_err[0]) {
         c->h_err[0] = 0;
         return set_err(c, -EIO, "device reported a look-back timeout");
@@ -533,9 +594,11 @@ int cop_sync(cop_ctx *c)
 int cop_poll(cop_ctx *c)
 {
     if (!c) return -EINVAL;
-    hipError_t e = hipStreamQuery(c->stream);
-    if (e == hipErrorNotReady) return -EAGAIN;
-    if (e != hipSuccess) return set_err(c, -EIO, "stream: %s", hipGetErrorString(e));
+    for (int l = 0; l < c->n_lanes; l++) {
+        hipError_t e = hipStreamQuery(c->lane[l].s);
+        if (e == hipErrorNotReady) return -EAGAIN;
+        if (e != hipSuccess) return set_err(c, -EIO, "stream: %s", hipGetErrorString(e));
+    }
     if (c->h_err[0]) {
         c->h_err[0] = 0;
         return set_err(c, -EIO, "device reported a look-back timeout");
@@ -569,6 +632,7 @@ int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_re
         HIPCHK(c, hipMalloc(&c->d_fwdn, 16));
         c->stage_cap = cap;
     }
+    if (int rc0 = sync_lanes(c)) return rc0;   // the staging buffers may still be in use
     // gather the first 64 bytes of every packet (headers the pipeline reads)
     for (uint32_t i = 0; i < n; i++) memcpy(c->h_stage + (size_t)i * 64, pkt_data[i], 64);
     HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, (size_t)n * 64, hipMemcpyHostToDevice, c->stream));
@@ -580,7 +644,7 @@ int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_re
     b.results = c->d_res;
     b.fwd_idx = fwd_idx ? c->d_fwd : nullptr;
     b.fwd_count = (fwd_idx || fwd_count) ? c->d_fwdn : nullptr;
-    int rc = cop_submit(c, &b, 1);
+    int rc = submit_on(c, c->lane[0], &b, 1);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(results, c->d_res, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
     uint32_t cnt = 0;
@@ -594,11 +658,72 @@ int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_re
     return 0;
 }
 
+static int lane_finish(cop_ctx *c, Lane &L, cop_result *results)
+{
+    if (!L.busy) return 0;
+    HIPCHK(c, hipEventSynchronize(L.done));
+    memcpy(results + L.first, L.h_res, (size_t)L.n * sizeof(cop_result));
+    L.busy = false;
+    return 0;
+}
+
+int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n, uint32_t batch,
+                            cop_result *results)
+{
+    if (!c || (n && (!pkt_data || !results)) || batch == 0) return -EINVAL;
+    if (batch > c->cfg.max_batch) return set_err(c, -EINVAL, "batch %u > max_batch", batch);
+    if (int rc = sync_lanes(c)) return rc;
+    for (int l = 0; l < c->n_lanes; l++) {
+        Lane &L = c->lane[l];
+        if (L.cap >= batch) continue;
+        if (L.h_stage) (void)hipHostFree(L.h_stage);
+        if (L.h_res) (void)hipHostFree(L.h_res);
+        if (L.d_stage) (void)hipFree(L.d_stage);
+        if (L.d_res) (void)hipFree(L.d_res);
+        L.h_stage = L.d_stage = nullptr;
+        L.h_res = L.d_res = nullptr;
+        L.cap = 0;
+        HIPCHK(c, hipHostMalloc(&L.h_stage, (size_t)batch * 64, hipHostMallocDefault));
+        HIPCHK(c, hipHostMalloc(&L.h_res, (size_t)batch * 8, hipHostMallocDefault));
+        HIPCHK(c, hipMalloc(&L.d_stage, (size_t)batch * 64));
+        HIPCHK(c, hipMalloc(&L.d_res, (size_t)batch * 8));
+        L.cap = batch;
+    }
+    int lane = 0;
+    for (uint64_t first = 0; first < n; first += batch) {
+        Lane &L = c->lane[lane];
+        lane = (lane + 1) % c->n_lanes;
+        if (int rc = lane_finish(c, L, results)) return rc;
+        const uint32_t k = (uint32_t)((n - first) < batch ? (n - first) : batch);
+        // host gather of the 64-byte header lines (overlaps the other lanes)
+        for (uint32_t i = 0; i < k; i++) memcpy(L.h_stage + (size_t)i * 64, pkt_data[first + i], 64);
+        HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * 64, hipMemcpyHostToDevice, L.s));
+        cop_batch b;
+        memset(&b, 0, sizeof(b));
+        b.pkts = L.d_stage;
+        b.n = k;
+        b.stride = 64;
+        b.results = L.d_res;
+        if (int rc = submit_on(c, L, &b, 1)) return rc;
+        HIPCHK(c, hipMemcpyAsync(L.h_res, L.d_res, (size_t)k * 8, hipMemcpyDeviceToHost, L.s));
+        HIPCHK(c, hipEventRecord(L.done, L.s));
+        L.busy = true;
+        L.first = first;
+        L.n = k;
+    }
+    for (int l = 0; l < c->n_lanes; l++)
+        if (int rc = lane_finish(c, c->lane[l], results)) return rc;
+    if (c->h_err[0]) {
+        c->h_err[0] = 0;
+        return set_err(c, -EIO, "device reported a look-back timeout");
+    }
+    return 0;
+}
+
 int cop_counters_read(cop_ctx *c, cop_counters *out, int reset)
 {
     if (!c || !out) return -EINVAL;
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = sync_lanes(c)) return rc;
     std::vector<uint64_t> sh((size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS);
     HIPCHK(c, hipMemcpy(sh.data(), c->counters, sh.size() * 8, hipMemcpyDeviceToHost));
     uint64_t sum[COP_N_COUNTERS] = {0};
@@ -645,6 +770,7 @@ int cop_host_free_pinned(cop_ctx *c, void *hptr)
 int cop_memcpy_h2d(cop_ctx *c, void *dst, const void *src, size_t bytes)
 {
     if (!c) return -EINVAL;
+    if (int rc = sync_lanes(c)) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -654,6 +780,7 @@ int cop_memcpy_h2d(cop_ctx *c, void *dst, const void *src, size_t bytes)
 int cop_memcpy_d2h(cop_ctx *c, void *dst, const void *src, size_t bytes)
 {
     if (!c) return -EINVAL;
+    if (int rc = sync_lanes(c)) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -663,6 +790,7 @@ int cop_memcpy_d2h(cop_ctx *c, void *dst, const void *src, size_t bytes)
 int cop_memcpy_d2d(cop_ctx *c, void *dst, const void *src, size_t bytes)
 {
     if (!c) return -EINVAL;
+    if (int rc = sync_lanes(c)) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -672,6 +800,7 @@ int cop_memcpy_d2d(cop_ctx *c, void *dst, const void *src, size_t bytes)
 int cop_memset_d(cop_ctx *c, void *dst, int value, size_t bytes)
 {
     if (!c) return -EINVAL;
+    if (int rc = sync_lanes(c)) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemsetAsync(dst, value, bytes, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -682,12 +811,17 @@ int cop_timer_start(cop_ctx *c)
 {
     if (!c) return -EINVAL;
     HIPCHK(c, hipEventRecord(c->t0, c->stream));
+    for (int l = 1; l < c->n_lanes; l++) HIPCHK(c, hipStreamWaitEvent(c->lane[l].s, c->t0, 0));
     return 0;
 }
 
 int cop_timer_stop(cop_ctx *c, double *ms)
 {
     if (!c || !ms) return -EINVAL;
+    for (int l = 1; l < c->n_lanes; l++) {
+        HIPCHK(c, hipEventRecord(c->lane[l].join, c->lane[l].s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->lane[l].join, 0));
+    }
     HIPCHK(c, hipEventRecord(c->t1, c->stream));
     HIPCHK(c, hipEventSynchronize(c->t1));
     float f = 0;
@@ -702,7 +836,7 @@ int cop_debug_stamps(cop_ctx *c, uint64_t *out, uint32_t max_words)
 {
     if (!c || !c->stamps) return -EINVAL;
     uint32_t n = max_words < COPK_STAMP_WG * 8 ? max_words : COPK_STAMP_WG * 8;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = sync_lanes(c)) return rc;
     HIPCHK(c, hipMemcpy(out, c->stamps, (size_t)n * 8, hipMemcpyDeviceToHost));
     return (int)n;
 }
@@ -717,7 +851,8 @@ int cop_launch_timing(cop_ctx *c, int enable)
 int cop_launch_timing_read(cop_ctx *c, double *mean_ms, uint64_t *n, int reset)
 {
     if (!c) return -EINVAL;
-    while (c->ev_count) harvest_one(c);
+    for (int l = 0; l < c->n_lanes; l++)
+        while (c->lane[l].ev_count) harvest_one(c, c->lane[l]);
     if (mean_ms) *mean_ms = c->ev_n ? c->ev_sum_ms / (double)c->ev_n : 0.0;
     if (n) *n = c->ev_n;
     if (reset) {

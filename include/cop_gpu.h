@@ -181,6 +181,7 @@ typedef struct cop_config {
     uint32_t max_batch;       /* packets per batch, default 262144 */
     uint32_t max_batches;     /* batches per cop_submit, default 32 */
     uint32_t flags;           /* COP_CFG_* */
+    uint32_t n_streams;       /* launch lanes (HIP streams) used round-robin, 1..4, default 2 */
     const uint16_t *routing_table; /* 65536 entries, or NULL = read_config default */
 } cop_config;
 
@@ -220,10 +221,12 @@ typedef struct cop_batch {
     uint32_t       *fwd_count; /* device pointer, 1 entry, or NULL */
 } cop_batch;
 
-/* Enqueue nb batches (nb <= max_batches) as ONE kernel launch on the
- * context's stream. Asynchronous: returns after the launch is queued. */
+/* Enqueue nb batches (nb <= max_batches) as ONE kernel launch on the next
+ * launch lane (stream) of the context, round-robin. Launches on different
+ * lanes may run concurrently. Asynchronous: returns once queued; outputs are
+ * valid after cop_sync. */
 int  cop_submit(cop_ctx *ctx, const cop_batch *batches, uint32_t nb);
-/* Block until everything submitted has completed. 0 or -EIO. */
+/* Block until everything submitted on every lane has completed. 0 or -EIO. */
 int  cop_sync(cop_ctx *ctx);
 /* Non-blocking: 0 when idle, -EAGAIN while work is in flight. */
 int  cop_poll(cop_ctx *ctx);
@@ -233,8 +236,17 @@ int  cop_poll(cop_ctx *ctx);
  * pipeline, hipMemcpyAsync D2H of results and forward list. Synchronous. */
 int  cop_process_host(cop_ctx *ctx, const void *const *pkt_data, uint32_t n,
                       cop_result *results, uint32_t *fwd_idx, uint32_t *fwd_count);
+/* Streaming form of the end-to-end path: n packets at host addresses
+ * pkt_data[i], in batches of `batch` (<= max_batch): the host gather of one
+ * batch overlaps the H2D copy, kernel and D2H copy of earlier batches on the
+ * other lanes. results[i] for every packet. Synchronous on return. */
+int  cop_process_host_stream(cop_ctx *ctx, const void *const *pkt_data, uint64_t n, uint32_t batch,
+                             cop_result *results);
 
 /* Counters (u64, device-resident, summed over every submitted packet).
+ * On the device they are kept in COP_COUNTER_SHARDS shards of
+ * COP_N_COUNTERS words (one 128-byte line each, to spread the atomics);
+ * cop_counters_read folds the shards.
  * pkt_total / pkt_not_ipv4 mirror struct firewall_pkt_stats
  * (firewall.h:56-61, incremented at firewall.c:184,188); pkt_accept /
  * pkt_drop are filled here although the reference never increments them. */
@@ -251,9 +263,11 @@ typedef struct cop_counters {
     uint64_t _rsvd[7];
 } cop_counters;
 #define COP_N_COUNTERS 16
+#define COP_COUNTER_SHARDS 64
 
 int  cop_counters_read(cop_ctx *ctx, cop_counters *out, int reset);
-/* Device address of the 16 u64 counters (for an RCCL all-reduce in place). */
+/* Device address of the COP_COUNTER_SHARDS x COP_N_COUNTERS u64 counter
+ * shards (an element-wise sum over GPUs preserves the per-shard layout). */
 void *cop_counters_device_ptr(cop_ctx *ctx);
 
 /* Device memory helpers so C callers need no HIP headers. */
@@ -266,7 +280,7 @@ int  cop_memcpy_d2h(cop_ctx *ctx, void *dst, const void *src, size_t bytes);
 int  cop_memcpy_d2d(cop_ctx *ctx, void *dst, const void *src, size_t bytes);
 int  cop_memset_d(cop_ctx *ctx, void *dst, int value, size_t bytes);
 
-/* Timing with HIP events on the context's stream. */
+/* Timing with HIP events: start/stop join every lane of the context. */
 int  cop_timer_start(cop_ctx *ctx);
 int  cop_timer_stop(cop_ctx *ctx, double *ms);
 /* When on, every cop_submit is bracketed by an event pair; the mean kernel

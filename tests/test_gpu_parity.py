@@ -230,3 +230,49 @@ def test_repeated_submits_epochs(gpu_ctx_factory):
     for _ in range(50):
         rg, fg, _ = gpu_run(ctx, pk, n, batches=3)
     assert_parity(rg, fg, ro, fo)
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 4])
+def test_process_host_stream_lanes(gpu_ctx_factory, lanes):
+    """Streaming end-to-end host path over mbuf-like scattered buffers."""
+    rules = fw1k()
+    ctx = setup_ctx(gpu_ctx_factory, rules, n_streams=lanes)
+    n = 50000
+    pk = cg.gen_trace(0x5EED0700, n, rules)
+    stride = 2176
+    pool = np.zeros(n * stride, dtype=np.uint8)
+    pool.reshape(n, stride)[:, 128:192] = pk.reshape(n, 64)
+    ptrs = (pool.ctypes.data + 128 + np.arange(n, dtype=np.uint64) * stride).astype(np.uint64)
+    fwo, _ = oracle_tables(rules)
+    ro, _, _ = orc.process(pk, n, stages=S | F, fw=fwo)
+    res = ctx.process_host_stream(ptrs, 8192)
+    assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
+
+
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_concurrent_lanes_many_submits(gpu_ctx_factory, lanes):
+    """Back-to-back submits spread over lanes (kernels may overlap): every
+    batch still gets exactly its own results and ordered forward list."""
+    rules = fw1k()
+    ctx = setup_ctx(gpu_ctx_factory, rules, n_streams=lanes)
+    B, P = 65536, 12
+    pk = cg.gen_trace(0x5EED0800, B * P, rules)
+    dp = ctx.alloc(pk.nbytes)
+    dp.upload(pk)
+    dr = ctx.alloc(B * P * 8)
+    df = ctx.alloc(B * P * 4)
+    dc = ctx.alloc(P * 4)
+    for rep in range(3):
+        for i in range(0, P, 3):
+            ctx.submit([cg.make_batch(dp.addr + (i + j) * B * 64, B, dr.addr + (i + j) * B * 8,
+                                      fwd_idx=df.addr + (i + j) * B * 4, fwd_count=dc.addr + (i + j) * 4)
+                        for j in range(3)])
+    ctx.sync()
+    res = dr.download(cg.RESULT_DT, B * P)
+    cnt = dc.download(np.uint32, P)
+    fwd = df.download(np.uint32, B * P)
+    fwo, _ = oracle_tables(rules)
+    ro, fo, _ = orc.process(pk, B * P, stages=S | F, fw=fwo)
+    assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
+    got = np.concatenate([fwd[i * B: i * B + cnt[i]] + i * B for i in range(P)])
+    assert np.array_equal(got, fo)

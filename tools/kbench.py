@@ -68,6 +68,9 @@ def main():
     }
     for ppt in (1, 4, 8):
         variants[f"fw_L16_p{ppt}"] = (S | F, 0, 16, True, (("COP_PPT", str(ppt)),))
+    for ns in (1, 2, 4):
+        variants[f"fw_L16_s{ns}"] = (S | F, 0, 16, True, (("COP_STREAMS", str(ns)),))
+        variants[f"fw_L32_s{ns}"] = (S | F, 0, 32, True, (("COP_STREAMS", str(ns)),))
     # timing-only ablations (COP_DBG bits: 1 no counter atomics, 2 static tiles, 4 no LDS staging)
     for dbg in (1, 2, 3, 7):
         variants[f"nc_dbg{dbg}"] = (S | F, 0, 16, False, (("COP_DBG", str(dbg)),))

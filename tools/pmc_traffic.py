@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the pipeline kernel from rocprofv3 PMC passes.
+
+Method (MI355X_MICROARCH.md §HBM, cdna_hip_programming.md §7): FETCH_SIZE
+and WRITE_SIZE are collected in separate --pmc passes (they do not fit one
+pass); both are in KiB per dispatch. On gfx950 FETCH_SIZE under-counts wide
+streaming reads by 2x and other widths are uncalibrated, so the read factor
+is calibrated here on tools/membench, whose kernels read a known byte count
+with the pipeline's exact access pattern (kA: dword@12 + dwordx3@24 per
+64-byte slot) and with dwordx4 streaming (kD).
+
+usage: pmc_traffic.py <fetch_bench.csv> <write_bench.csv> <fetch_mb.csv> <write_mb.csv> <out.json>
+"""
+import collections
+import csv
+import json
+import statistics
+import sys
+
+MB_PKTS = 5 << 20           # tools/membench: 5 Mi packets of 64 B
+MB_SLICE = 1 << 20          # its 1 Mi-packet slice runs
+
+
+def load(path):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        d[r["Kernel_Name"]].append((int(r["Grid_Size"]), float(r["Counter_Value"])))
+    return d
+
+
+def main():
+    fb, wb, fm, wm, out = sys.argv[1:6]
+    fetch_mb, write_mb = load(fm), load(wm)
+    # calibration on kA<4> (whole 320 MiB: 5 Mi packets) and kD (dwordx4)
+    cal = {}
+    for name, vals in fetch_mb.items():
+        if name.startswith("void kA<4>"):
+            cal["kA_strided_read_factor"] = (MB_PKTS * 64 / 1024) / statistics.median(v for _, v in vals)
+        if name.startswith("kD("):
+            cal["kD_stream_read_factor"] = (MB_PKTS * 64 / 1024) / statistics.median(v for _, v in vals)
+    for name, vals in write_mb.items():
+        if name.startswith("void kA<4>"):
+            cal["kA_dword_write_factor"] = (MB_PKTS * 4 / 1024) / statistics.median(v for _, v in vals)
+    rf = cal["kA_strided_read_factor"]
+    wf = cal["kA_dword_write_factor"]
+    fb_, wb_ = load(fb), load(wb)
+    res = {}
+    for name in fb_:
+        if "cop_pipeline" not in name:
+            continue
+        f = statistics.median(v for _, v in fb_[name])
+        w = statistics.median(v for _, v in wb_.get(name, [(0, 0.0)]))
+        res[name] = {"dispatches": len(fb_[name]), "fetch_kib_raw": f, "write_kib_raw": w,
+                     "read_bytes": f * 1024 * rf, "write_bytes": w * 1024 * wf,
+                     "hbm_bytes_per_launch": f * 1024 * rf + w * 1024 * wf}
+    main_k = max(res, key=lambda k: res[k]["dispatches"])
+    doc = {"kernel": main_k, "hbm_bytes_per_launch": res[main_k]["hbm_bytes_per_launch"],
+           "read_bytes_per_launch": res[main_k]["read_bytes"], "write_bytes_per_launch": res[main_k]["write_bytes"],
+           "calibration": cal, "kernels": res,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; KiB per dispatch; "
+                     "read factor calibrated on tools/membench kA (same access pattern, known bytes)"}
+    json.dump(doc, open(out, "w"), indent=1)
+    print(json.dumps({k: doc[k] for k in ("kernel", "hbm_bytes_per_launch", "calibration")}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
