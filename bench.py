@@ -56,10 +56,11 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=6400)
-    ap.add_argument("--warmup", type=int, default=640)
+    ap.add_argument("--steps", type=int, default=6720)
+    ap.add_argument("--warmup", type=int, default=960)
     ap.add_argument("--workload", default="fw1k", choices=sorted(WORKLOADS))
-    ap.add_argument("--per-launch", type=int, default=16, help="batches per kernel launch")
+    ap.add_argument("--per-launch", type=int, default=96, help="batches per kernel launch (ring submit)")
+    ap.add_argument("--streams", type=int, default=1, help="launch lanes (concurrent streams)")
     ap.add_argument("--pool-mib", type=int, default=400, help="distinct input bytes per GPU")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
@@ -68,7 +69,7 @@ def main():
     rank, world, local = copdist.env()
     W = WORKLOADS[args.workload]
     B = W["batch"]
-    Lb = max(1, min(args.per_launch, 32))
+    Lb = max(1, args.per_launch)
 
     cg.lib()   # load the HIP runtime the product links (before torch)
     dev = copdist.device_for(local, cg.device_count())
@@ -83,7 +84,7 @@ def main():
         fw_tab = cg.LpmTable(fw_rules, 1024, 24, True)                  # lpm_setup's own limits
     else:
         fw_tab = cg.LpmTable(fw_rules, W["fw"], 1 << 20, False)
-    ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32)
+    ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32, n_streams=args.streams)
     ctx.set_fw_table(fw_tab)
     if routes is not None:
         ctx.set_route_lpm(cg.LpmTable(routes, max(W["routes"], 1), 1 << 20, False))
@@ -115,20 +116,19 @@ def main():
             d_pkts.upload(pk, i * per_batch)
     log(f"[rank {rank}] pool: {P} batches x {B} pkts ({P * per_batch / 2**20:.0f} MiB) in {time.time() - t0:.1f}s")
 
-    def batch(i):
-        i %= P
-        if W["imix"]:
-            base = d_pkts.addr + i * per_batch
-            return cg.make_batch(base, B, d_res.addr + i * B * 8, offsets=base + slab.nbytes,
-                                 fwd_idx=d_fwd.addr + i * B * 4, fwd_count=d_cnt.addr + i * 4)
-        return cg.make_batch(d_pkts.addr + i * per_batch, B, d_res.addr + i * B * 8, stride=64,
-                             fwd_idx=d_fwd.addr + i * B * 4, fwd_count=d_cnt.addr + i * 4)
+    # the pool is a batch ring in HBM: one launch = Lb consecutive slots
+    Lb = min(Lb, P)
+    if W["imix"]:
+        ring = cg.make_ring(d_pkts, P, B, d_res, per_batch, offsets=d_pkts.addr + slab.nbytes,
+                            offsets_slot_words=per_batch // 4, fwd_idx=d_fwd, fwd_count=d_cnt)
+    else:
+        ring = cg.make_ring(d_pkts, P, B, d_res, per_batch, stride=64, fwd_idx=d_fwd, fwd_count=d_cnt)
 
     def run_steps(first, count):
         s = first
         while s < first + count:
             k = min(Lb, first + count - s)
-            ctx.submit([batch(s + j) for j in range(k)])
+            ctx.submit_ring(ring, s % P, k)
             s += k
 
     # ---- warmup, then exactly K timed steps ----
@@ -164,7 +164,7 @@ def main():
     achieved = alg_bytes / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
 
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_L{Lb}.json")
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_L{Lb}_s{args.streams}.json")
     if os.path.exists(tpath):
         try:
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
@@ -189,6 +189,7 @@ def main():
             "description": W["desc"],
             "batch": B,
             "batches_per_launch": Lb,
+            "streams": args.streams,
             "fw_rules": W["fw"],
             "route_prefixes": W["routes"],
             "pkt_layout": "imix slab + u32 offsets" if W["imix"] else "64B slots",
@@ -218,7 +219,10 @@ def main():
         ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=W["fw"] <= 1000)
         ns = 131072
         trace = cg.gen_trace(0x5EED0001, ns, fw_rules, None)   # configs[0] seed: CPU reference case
-        rate, pk, secs = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget, 1, 0)
+        # pin to the last core this process may use (core 0 also serves this
+        # process's main thread and the driver's interrupts)
+        core = max(os.sched_getaffinity(0))
+        rate, pk, secs = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget, 1, core)
         out["cpu_baseline"] = {
             "value": round(rate, 3),
             "unit": "Mpkt/s",
@@ -226,7 +230,7 @@ def main():
             "kind": "port",
             "sample": (f"{pk} packets through the restated coprocessor() loop (burst 32, 16384-slot "
                        f"SPSC ring, 2176 B mbufs, DIR-24-8 firewall, {W['fw']} rules), "
-                       f"{secs:.1f} s on 1 pinned core"),
+                       f"{secs:.1f} s on 1 pinned core (cpu {core})"),
         }
         log(f"[rank 0] cpu baseline {rate:.1f} Mpkt/s on 1 core ({pk} pkts)")
 

@@ -64,6 +64,13 @@ class Batch(Structure):
                 ("fwd_idx", c_void_p), ("fwd_count", c_void_p)]
 
 
+class BatchRing(Structure):
+    _fields_ = [("pkts", c_void_p), ("offsets", c_void_p), ("results", c_void_p), ("fwd_idx", c_void_p),
+                ("fwd_count", c_void_p), ("pkts_slot_bytes", c_uint64), ("offsets_slot_words", c_uint64),
+                ("results_slot", c_uint64), ("fwd_slot", c_uint64), ("n_slots", c_uint32), ("n", c_uint32),
+                ("stride", c_uint32), ("data_off", c_uint32)]
+
+
 class TraceOpts(Structure):
     _fields_ = [("n_ports", c_uint32), ("pct_non_ipv4", c_uint32), ("pct_bad_version", c_uint32),
                 ("pct_unknown_dst", c_uint32), ("pct_vport_dst", c_uint32),
@@ -96,6 +103,7 @@ SIGNATURES = {
     "cop_set_routing_table": (c_int, [c_void_p, c_void_p]),
     "cop_load_fw_rules_file": (c_int, [c_void_p, c_char_p, POINTER(LpmConfig), POINTER(LpmReport)]),
     "cop_submit": (c_int, [c_void_p, POINTER(Batch), c_uint32]),
+    "cop_submit_ring": (c_int, [c_void_p, POINTER(BatchRing), c_uint32, c_uint32]),
     "cop_sync": (c_int, [c_void_p]),
     "cop_poll": (c_int, [c_void_p]),
     "cop_process_host": (c_int, [c_void_p, POINTER(c_void_p), c_uint32, c_void_p, c_void_p, c_void_p]),
@@ -383,6 +391,9 @@ class Context:
         arr = (Batch * len(batches))(*batches)
         _check(lib().cop_submit(self.handle, arr, len(batches)), self, "submit")
 
+    def submit_ring(self, ring: BatchRing, first_slot: int, count: int):
+        _check(lib().cop_submit_ring(self.handle, byref(ring), first_slot, count), self, "submit_ring")
+
     def sync(self):
         _check(lib().cop_sync(self.handle), self, "sync")
 
@@ -430,6 +441,23 @@ class Context:
         _check(lib().cop_launch_timing_read(self.handle, byref(ms), byref(n), 1 if reset else 0), self,
                "launch_timing_read")
         return ms.value, n.value
+
+
+def make_ring(pkts, n_slots: int, n: int, results, pkts_slot_bytes: int, results_slot: int = 0,
+              fwd_idx=None, fwd_slot: int = 0, fwd_count=None, stride: int = 64, offsets=None,
+              offsets_slot_words: int = 0, data_off: int = 0) -> BatchRing:
+    def addr(x):
+        if x is None:
+            return None
+        return x.addr if isinstance(x, DeviceBuffer) else int(x)
+    r = BatchRing()
+    r.pkts, r.offsets, r.results = addr(pkts), addr(offsets), addr(results)
+    r.fwd_idx, r.fwd_count = addr(fwd_idx), addr(fwd_count)
+    r.pkts_slot_bytes, r.offsets_slot_words = pkts_slot_bytes, offsets_slot_words
+    r.results_slot = results_slot or n
+    r.fwd_slot = fwd_slot or n
+    r.n_slots, r.n, r.stride, r.data_off = n_slots, n, stride, data_off
+    return r
 
 
 def make_batch(pkts: DeviceBuffer | int, n: int, results: DeviceBuffer | int, stride: int = 64,

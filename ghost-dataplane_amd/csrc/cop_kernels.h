@@ -8,6 +8,7 @@
 
 #define COPK_BLOCK 256
 #define COPK_MAXB 32
+#define COPK_MAX_LAUNCH_BATCHES 1024   /* ring launches; ticket lines per lane buffer */
 #define COPK_COUNTER_SHARDS 64   /* 16 u64 per shard (128 B) */
 static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_LDS_MISC_WORDS 80
@@ -39,11 +40,22 @@ struct CopKBatch {
     uint32_t ntiles;
 };
 
+struct CopKRing {
+    const uint8_t *pkts;
+    const uint32_t *offsets;
+    void *results;
+    uint32_t *fwd_idx;
+    uint32_t *fwd_count;
+    unsigned long long pkts_slot_bytes, offsets_slot_words, results_slot, fwd_slot;
+    uint32_t n_slots, first, n, stride, data_off;
+};
+
 struct CopKParams {
-    CopKBatch b[COPK_MAXB];
+    CopKBatch b[COPK_MAXB];                  // descriptor mode (ring == 0)
     uint32_t tile_begin[COPK_MAXB];          // first blockIdx of each batch
     uint32_t look_begin[COPK_MAXB];          // look-back word offset of each batch
-    unsigned long long ticket_base[COPK_MAXB];
+    CopKRing rg;                             // ring mode (ring == 1): batch b = slot first+b
+    uint32_t ring;
     uint32_t nb;
     uint32_t ntiles;
     uint32_t uniform_ntiles;  // tiles per batch when all batches are equal, else 0
@@ -67,7 +79,9 @@ struct CopKParams {
     // LDS carve (u32 words)
     uint32_t lds_fw_off, lds_lpm_off, lds_misc_off;
     // ordering / accounting state
-    unsigned long long *tickets;   // COPK_MAXB counters, one 128-byte line each
+    unsigned long long *tickets;   // one counter per batch, one 128-byte line each (zero at launch)
+    unsigned long long *zero_tickets;  // the lane's other ticket buffer: zeroed by this launch
+    uint32_t zero_lines;               // its dirty lines
     unsigned long long *look;
     unsigned long long *counters;
     uint32_t *err;

@@ -121,7 +121,29 @@ __global__ __launch_bounds__(BLOCK) void cop_pipeline(const CopKParams p)
         for (int q = 1; q < COPK_MAXB; q++) b += (q < (int)p.nb && p.tile_begin[q] <= g) ? 1u : 0u;
     }
     b = __builtin_amdgcn_readfirstlane(b);
-    const CopKBatch B = p.b[b];
+    CopKBatch B;
+    uint32_t look_off;
+    if (p.ring) {
+        const uint32_t slot = (p.rg.first + b) % p.rg.n_slots;   // count may exceed n_slots
+        B.pkts = p.rg.pkts + (size_t)slot * p.rg.pkts_slot_bytes;
+        B.offsets = p.rg.offsets ? p.rg.offsets + (size_t)slot * p.rg.offsets_slot_words : nullptr;
+        B.results = (uint2 *)p.rg.results + (size_t)slot * p.rg.results_slot;
+        B.fwd_idx = p.rg.fwd_idx ? p.rg.fwd_idx + (size_t)slot * p.rg.fwd_slot : nullptr;
+        B.fwd_count = p.rg.fwd_count ? p.rg.fwd_count + slot : nullptr;
+        B.n = p.rg.n;
+        B.stride = p.rg.stride;
+        B.data_off = p.rg.data_off;
+        B.ntiles = p.uniform_ntiles;
+        look_off = b * p.uniform_ntiles;
+    } else {
+        B = p.b[b];
+        look_off = p.look_begin[b];
+    }
+
+    // ---- zero the lane's other ticket buffer for the next launch on this
+    // lane (stream order puts that launch after this one completes) ----
+    for (uint32_t line = g; line < p.zero_lines; line += gridDim.x)
+        if (tid < 16) p.zero_tickets[line * 16 + tid] = 0ull;
 
     // ---- tile index inside the batch: this batch's ticket counter (or the
     // static order when no look-back runs: p.compact == 0) ----
@@ -144,11 +166,11 @@ __global__ __launch_bounds__(BLOCK) void cop_pipeline(const CopKParams p)
     }
     uint32_t j;
     if (dyn) {
-        if (tid == 0) *s_tile = (uint32_t)(tk - p.ticket_base[b]);
+        if (tid == 0) *s_tile = (uint32_t)tk;
         __syncthreads();
         j = __builtin_amdgcn_readfirstlane(*s_tile);
     } else {
-        j = g - p.tile_begin[b];
+        j = p.ring ? g - b * p.uniform_ntiles : g - p.tile_begin[b];
     }
     const uint32_t base = j * TILE;
     STAMP(1);
@@ -313,7 +335,7 @@ __global__ __launch_bounds__(BLOCK) void cop_pipeline(const CopKParams p)
             const uint32_t agg = __shfl(inc, NQ - 1);
             if (lane < NQ) s_cnt[lane] = inc - c;
             const unsigned long long ep = (unsigned long long)p.epoch << 32;
-            unsigned long long *look = p.look + p.look_begin[b];
+            unsigned long long *look = p.look + look_off;
             uint32_t excl = 0;
             if (j == 0) {
                 if (lane == 0) lb_store(&look[j], ep | (2ull << 30) | agg);

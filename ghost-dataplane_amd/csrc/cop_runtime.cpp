@@ -38,9 +38,13 @@ struct DevLpm {
 
 struct Lane {
     hipStream_t s = nullptr;
-    unsigned long long *tickets = nullptr;          // COPK_MAXB x 16 u64
-    unsigned long long tbase[COPK_MAXB] = {0};
+    // two ticket buffers (COPK_MAX_LAUNCH_BATCHES lines of 16 u64): launch k
+    // on this lane draws from buffer k%2 and zeroes the other one's dirty lines
+    unsigned long long *tickets[2] = {nullptr, nullptr};
+    uint32_t dirty[2] = {0, 0};
+    int parity = 0;
     unsigned long long *look = nullptr;
+    uint32_t look_cap = 0;
     uint32_t epoch = 0;
     hipEvent_t ev[TIMING_SLOTS][2];
     int ev_head = 0, ev_count = 0, ev_created = 0;
@@ -170,7 +174,8 @@ void cop_destroy(cop_ctx *c)
     if (c->t1) (void)hipEventDestroy(c->t1);
     for (int l = 0; l < MAX_LANES; l++) {
         Lane &L = c->lane[l];
-        if (L.tickets) (void)hipFree(L.tickets);
+        for (int q = 0; q < 2; q++)
+            if (L.tickets[q]) (void)hipFree(L.tickets[q]);
         if (L.look) (void)hipFree(L.look);
         for (int i = 0; i < L.ev_created; i++) {
             (void)hipEventDestroy(L.ev[i][0]);
@@ -295,10 +300,13 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     for (int l = 0; l < c->n_lanes; l++) {
         Lane &L = c->lane[l];
         CREATE_CHK(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
-        CREATE_CHK(hipMalloc(&L.tickets, COPK_MAXB * 16 * sizeof(unsigned long long)));
-        CREATE_CHK(hipMemset(L.tickets, 0, COPK_MAXB * 16 * sizeof(unsigned long long)));
+        for (int q = 0; q < 2; q++) {
+            CREATE_CHK(hipMalloc(&L.tickets[q], COPK_MAX_LAUNCH_BATCHES * 16 * sizeof(unsigned long long)));
+            CREATE_CHK(hipMemset(L.tickets[q], 0, COPK_MAX_LAUNCH_BATCHES * 16 * sizeof(unsigned long long)));
+        }
         CREATE_CHK(hipMalloc(&L.look, (size_t)c->look_cap * 8));
         CREATE_CHK(hipMemset(L.look, 0, (size_t)c->look_cap * 8));
+        L.look_cap = c->look_cap;
         CREATE_CHK(hipEventCreateWithFlags(&L.join, hipEventDisableTiming));
         CREATE_CHK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
         for (int i = 0; i < TIMING_SLOTS; i++) {
@@ -450,6 +458,7 @@ static void harvest_one(cop_ctx *c, Lane &L)
 }
 
 static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb);
+static int pick_mode(const cop_ctx *c, const DevLpm &t, bool enabled, bool force_dir);
 
 int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
 {
@@ -460,70 +469,41 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
     return submit_on(c, L, batches, nb);
 }
 
-static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb)
+static int choose_ppt(const cop_ctx *c, uint64_t total)
 {
-    if (nb > c->cfg.max_batches) return set_err(c, -EINVAL, "nb %u > max_batches", nb);
-    const uint32_t stages = c->cfg.stages;
-    const bool fw_on = (stages & COP_STAGE_FW) != 0;
-    const bool lpm_on = (stages & COP_STAGE_LPM) != 0;
-    int fw_mode = pick_mode(c, c->fw, fw_on, (c->cfg.flags & COP_CFG_FW_FORCE_DIR24) != 0);
-    int lpm_mode = pick_mode(c, c->lpm, lpm_on, (c->cfg.flags & COP_CFG_LPM_FORCE_DIR24) != 0);
-
-    CopKParams p;
-    memset(&p, 0, sizeof(p));
-    uint64_t total = 0;
-    bool imix = batches[0].offsets != nullptr;
-    bool compact = false;
-    for (uint32_t i = 0; i < nb; i++) {
-        const cop_batch &b = batches[i];
-        if ((b.offsets != nullptr) != imix)
-            return set_err(c, -EINVAL, "batches in one submit must all be slot or all IMIX");
-        if (b.n > c->cfg.max_batch) return set_err(c, -EINVAL, "batch %u: n %u > max_batch", i, b.n);
-        if (b.n && (!b.pkts || !b.results)) return set_err(c, -EINVAL, "batch %u: null pointer", i);
-        if (((uintptr_t)b.pkts & 15) || (b.data_off & 15) || (!imix && (b.stride & 15)) ||
-            (!imix && b.stride < 36))
-            return set_err(c, -EINVAL, "batch %u: packet starts must be 16-byte aligned", i);
-        if ((uintptr_t)b.results & 7) return set_err(c, -EINVAL, "batch %u: results misaligned", i);
-        total += b.n;
-        if (b.fwd_idx || b.fwd_count) compact = true;
-    }
-    if (c->cfg.flags & COP_CFG_NO_COMPACT) compact = false;
-    // tile size: the largest of 256 * {8, 4, 1} packets that still gives
-    // at least one tile per CU (fewer tiles = fewer ticket / look-back steps)
+    // tile size: the largest of 256 * {8, 4, 1} packets that still gives at
+    // least one tile per CU (fewer tiles = fewer ticket / look-back steps)
     int ppt = 1;
     if (total >= (uint64_t)COPK_BLOCK * 8 * c->ncu) ppt = 8;
     else if (total >= (uint64_t)COPK_BLOCK * 4 * c->ncu) ppt = 4;
     if (c->ppt_override) ppt = c->ppt_override;
-    const uint32_t tile = COPK_BLOCK * ppt;
-    uint32_t ntiles = 0;
-    for (uint32_t i = 0; i < nb; i++) {
-        const cop_batch &b = batches[i];
-        CopKBatch &d = p.b[i];
-        d.pkts = (const uint8_t *)b.pkts;
-        d.offsets = b.offsets;
-        d.results = b.results;
-        d.fwd_idx = compact ? b.fwd_idx : nullptr;
-        d.fwd_count = compact ? b.fwd_count : nullptr;
-        d.n = b.n;
-        d.stride = b.stride;
-        d.data_off = b.data_off;
-        d.ntiles = b.n ? (b.n + tile - 1) / tile : 1;   // an empty batch still reports count 0
-        p.tile_begin[i] = ntiles;
-        p.look_begin[i] = ntiles;
-        p.ticket_base[i] = L.tbase[i];
-        ntiles += d.ntiles;
+    return ppt;
+}
+
+// Fill the table / state part of the parameters and launch on lane L.
+// p.b / p.rg, p.nb, p.ntiles, p.uniform_ntiles and p.compact are set by the caller.
+static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, int ppt, uint32_t nb_used)
+{
+    const uint32_t stages = c->cfg.stages;
+    int fw_mode = pick_mode(c, c->fw, (stages & COP_STAGE_FW) != 0, (c->cfg.flags & COP_CFG_FW_FORCE_DIR24) != 0);
+    int lpm_mode =
+        pick_mode(c, c->lpm, (stages & COP_STAGE_LPM) != 0, (c->cfg.flags & COP_CFG_LPM_FORCE_DIR24) != 0);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (p.ntiles > L.look_cap) {
+        // grow this lane's look-back words (stream order: free after its work)
+        HIPCHK(c, hipStreamSynchronize(L.s));
+        HIPCHK(c, hipFree(L.look));
+        L.look = nullptr;
+        L.look_cap = 0;
+        HIPCHK(c, hipMalloc(&L.look, (size_t)p.ntiles * 8));
+        HIPCHK(c, hipMemset(L.look, 0, (size_t)p.ntiles * 8));
+        L.look_cap = p.ntiles;
+        L.epoch = 0;
     }
-    if (ntiles > c->look_cap) return set_err(c, -EINVAL, "too many tiles");
-    p.nb = nb;
-    p.ntiles = ntiles;
-    p.uniform_ntiles = p.b[0].ntiles;
-    for (uint32_t i = 1; i < nb; i++)
-        if (p.b[i].ntiles != p.b[0].ntiles) p.uniform_ntiles = 0;
     p.stages = stages;
     p.n_ports = c->cfg.n_ports;
-    p.compact = compact ? 1u : 0u;
     if (++L.epoch == 0) {
-        HIPCHK(c, hipMemsetAsync(L.look, 0, (size_t)c->look_cap * 8, L.s));
+        HIPCHK(c, hipMemsetAsync(L.look, 0, (size_t)L.look_cap * 8, L.s));
         L.epoch = 1;
     }
     p.epoch = L.epoch;
@@ -551,33 +531,128 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb)
     off += COPK_LDS_MISC_WORDS;
     const uint32_t lds_bytes = off * 4;
     if (lds_bytes > 160 * 1024) return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_bytes);
-    p.tickets = L.tickets;
+    // tickets: draw from buffer `parity`, zero the other buffer's dirty lines
+    const int q = L.parity;
+    p.tickets = L.tickets[q];
+    p.zero_tickets = L.tickets[q ^ 1];
+    p.zero_lines = L.dirty[q ^ 1];
     p.look = L.look;
     p.counters = c->counters;
     p.err = c->d_err;
     p.stamps = c->stamps;
-    if ((c->dbg & 8u) && ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
-    const uint32_t grid = ntiles;   // one tile per workgroup
-    if (compact && !(c->dbg & 2u))
-        for (uint32_t i = 0; i < nb; i++) L.tbase[i] += p.b[i].ntiles;
+    if ((c->dbg & 8u) && p.ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
+    const uint32_t grid = p.ntiles;   // one tile per workgroup
 
-    HIPCHK(c, hipSetDevice(c->device));
     if (c->timing) {
         if (L.ev_count == TIMING_SLOTS) harvest_one(c, L);
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][0], L.s));
     }
     hipError_t e = copk_launch(&p, fw_mode, lpm_mode, imix ? 1 : 0, ppt, grid, lds_bytes, L.s);
-    if (e != hipSuccess) {
-        if (compact && !(c->dbg & 2u))
-            for (uint32_t i = 0; i < nb; i++) L.tbase[i] -= p.b[i].ntiles;
-        return set_err(c, -EIO, "launch: %s", hipGetErrorString(e));
-    }
+    if (e != hipSuccess) return set_err(c, -EIO, "launch: %s", hipGetErrorString(e));
+    L.dirty[q ^ 1] = 0;
+    L.dirty[q] = (p.compact && !(c->dbg & 2u)) ? nb_used : 0;
+    L.parity = q ^ 1;
     if (c->timing) {
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][1], L.s));
         L.ev_head = (L.ev_head + 1) % TIMING_SLOTS;
         L.ev_count++;
     }
     return 0;
+}
+
+static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb)
+{
+    if (nb > c->cfg.max_batches) return set_err(c, -EINVAL, "nb %u > max_batches", nb);
+    CopKParams p;
+    memset(&p, 0, sizeof(p));
+    uint64_t total = 0;
+    bool imix = batches[0].offsets != nullptr;
+    bool compact = false;
+    for (uint32_t i = 0; i < nb; i++) {
+        const cop_batch &b = batches[i];
+        if ((b.offsets != nullptr) != imix)
+            return set_err(c, -EINVAL, "batches in one submit must all be slot or all IMIX");
+        if (b.n > c->cfg.max_batch) return set_err(c, -EINVAL, "batch %u: n %u > max_batch", i, b.n);
+        if (b.n && (!b.pkts || !b.results)) return set_err(c, -EINVAL, "batch %u: null pointer", i);
+        if (((uintptr_t)b.pkts & 15) || (b.data_off & 15) || (!imix && (b.stride & 15)) ||
+            (!imix && b.stride < 36))
+            return set_err(c, -EINVAL, "batch %u: packet starts must be 16-byte aligned", i);
+        if ((uintptr_t)b.results & 7) return set_err(c, -EINVAL, "batch %u: results misaligned", i);
+        total += b.n;
+        if (b.fwd_idx || b.fwd_count) compact = true;
+    }
+    if (c->cfg.flags & COP_CFG_NO_COMPACT) compact = false;
+    const int ppt = choose_ppt(c, total);
+    const uint32_t tile = COPK_BLOCK * ppt;
+    uint32_t ntiles = 0;
+    for (uint32_t i = 0; i < nb; i++) {
+        const cop_batch &b = batches[i];
+        CopKBatch &d = p.b[i];
+        d.pkts = (const uint8_t *)b.pkts;
+        d.offsets = b.offsets;
+        d.results = b.results;
+        d.fwd_idx = compact ? b.fwd_idx : nullptr;
+        d.fwd_count = compact ? b.fwd_count : nullptr;
+        d.n = b.n;
+        d.stride = b.stride;
+        d.data_off = b.data_off;
+        d.ntiles = b.n ? (b.n + tile - 1) / tile : 1;   // an empty batch still reports count 0
+        p.tile_begin[i] = ntiles;
+        p.look_begin[i] = ntiles;
+        ntiles += d.ntiles;
+    }
+    p.ring = 0;
+    p.nb = nb;
+    p.ntiles = ntiles;
+    p.uniform_ntiles = p.b[0].ntiles;
+    for (uint32_t i = 1; i < nb; i++)
+        if (p.b[i].ntiles != p.b[0].ntiles) p.uniform_ntiles = 0;
+    p.compact = compact ? 1u : 0u;
+    return launch_on(c, L, p, imix, ppt, nb);
+}
+
+int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, uint32_t count)
+{
+    if (!c || !r) return -EINVAL;
+    if (count == 0) return 0;
+    if (count > COPK_MAX_LAUNCH_BATCHES || r->n_slots == 0 || first_slot >= r->n_slots)
+        return set_err(c, -EINVAL, "ring: count %u / first %u / n_slots %u", count, first_slot, r->n_slots);
+    if (r->n > c->cfg.max_batch) return set_err(c, -EINVAL, "ring: n %u > max_batch", r->n);
+    const bool imix = r->offsets != nullptr;
+    if (r->n && (!r->pkts || !r->results)) return set_err(c, -EINVAL, "ring: null pointer");
+    if (((uintptr_t)r->pkts & 15) || (r->pkts_slot_bytes & 15) || (r->data_off & 15) ||
+        (!imix && ((r->stride & 15) || r->stride < 36)))
+        return set_err(c, -EINVAL, "ring: packet starts must be 16-byte aligned");
+    if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < r->n))
+        return set_err(c, -EINVAL, "ring: slot sizes smaller than n");
+    bool compact = (r->fwd_idx || r->fwd_count) && !(c->cfg.flags & COP_CFG_NO_COMPACT);
+    const int ppt = choose_ppt(c, (uint64_t)r->n * count);
+    const uint32_t tile = COPK_BLOCK * ppt;
+    const uint32_t tpb = r->n ? (r->n + tile - 1) / tile : 1;
+    CopKParams p;
+    memset(&p, 0, sizeof(p));
+    p.ring = 1;
+    p.rg.pkts = (const uint8_t *)r->pkts;
+    p.rg.offsets = r->offsets;
+    p.rg.results = r->results;
+    p.rg.fwd_idx = compact ? r->fwd_idx : nullptr;
+    p.rg.fwd_count = compact ? r->fwd_count : nullptr;
+    p.rg.pkts_slot_bytes = r->pkts_slot_bytes;
+    p.rg.offsets_slot_words = r->offsets_slot_words;
+    p.rg.results_slot = r->results_slot;
+    p.rg.fwd_slot = r->fwd_slot;
+    p.rg.n_slots = r->n_slots;
+    p.rg.first = first_slot;
+    p.rg.n = r->n;
+    p.rg.stride = r->stride;
+    p.rg.data_off = r->data_off;
+    p.nb = count;
+    p.ntiles = tpb * count;
+    p.uniform_ntiles = tpb;
+    p.compact = compact ? 1u : 0u;
+    Lane &L = c->lane[c->next_lane];
+    c->next_lane = (c->next_lane + 1) % c->n_lanes;
+    return launch_on(c, L, p, imix, ppt, count);
 }
 
 int cop_sync(cop_ctx *c)

@@ -226,6 +226,35 @@ typedef struct cop_batch {
  * lanes may run concurrently. Asynchronous: returns once queued; outputs are
  * valid after cop_sync. */
 int  cop_submit(cop_ctx *ctx, const cop_batch *batches, uint32_t nb);
+/* A ring of equally shaped batch slots resident in device memory (a batch
+ * ring buffer in HBM). Slot s: packets at pkts + s*pkts_slot_bytes (packet i
+ * at + i*stride + data_off, or, when offsets != NULL, at + offsets_s[i] +
+ * data_off with offsets_s = offsets + s*offsets_slot_words), records at
+ * results + s*results_slot, forward list at fwd_idx + s*fwd_slot (may be
+ * NULL), its length at fwd_count[s] (may be NULL). */
+typedef struct cop_batch_ring {
+    const void     *pkts;
+    const uint32_t *offsets;
+    cop_result     *results;
+    uint32_t       *fwd_idx;
+    uint32_t       *fwd_count;
+    uint64_t        pkts_slot_bytes;
+    uint64_t        offsets_slot_words;
+    uint64_t        results_slot;      /* records per slot (>= n) */
+    uint64_t        fwd_slot;          /* forward-list entries per slot (>= n) */
+    uint32_t        n_slots;
+    uint32_t        n;                 /* packets per batch */
+    uint32_t        stride;
+    uint32_t        data_off;
+} cop_batch_ring;
+
+#define COP_MAX_RING_BATCHES 1024u
+
+/* Enqueue `count` (<= COP_MAX_RING_BATCHES) consecutive slots starting at
+ * first_slot (wrapping at n_slots) as ONE kernel launch on the next lane.
+ * Per-batch semantics are exactly those of cop_submit. */
+int  cop_submit_ring(cop_ctx *ctx, const cop_batch_ring *ring, uint32_t first_slot, uint32_t count);
+
 /* Block until everything submitted on every lane has completed. 0 or -EIO. */
 int  cop_sync(cop_ctx *ctx);
 /* Non-blocking: 0 when idle, -EAGAIN while work is in flight. */

@@ -276,3 +276,62 @@ def test_concurrent_lanes_many_submits(gpu_ctx_factory, lanes):
     assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
     got = np.concatenate([fwd[i * B: i * B + cnt[i]] + i * B for i in range(P)])
     assert np.array_equal(got, fo)
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_ring_submit_wrapping(gpu_ctx_factory, lanes):
+    """cop_submit_ring: slots at constant strides, launches that wrap the
+    ring, with ragged n (not a tile multiple); per-slot parity."""
+    rules = fw1k()
+    routes = routes100k(n=20000)
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L, n_streams=lanes)
+    n, P = 20000 + 77, 9
+    slot_bytes = ((n * 64 + 4095) // 4096) * 4096
+    pk = cg.gen_trace(0x5EED0900, n * P, rules, routes)
+    dp = ctx.alloc(slot_bytes * P)
+    for s in range(P):
+        dp.upload(pk[s * n * 64:(s + 1) * n * 64], s * slot_bytes)
+    res_slot = n + 13
+    dr = ctx.alloc(res_slot * P * 8)
+    df = ctx.alloc(res_slot * P * 4)
+    dc = ctx.alloc(P * 4)
+    ring = cg.make_ring(dp, P, n, dr, slot_bytes, results_slot=res_slot, fwd_idx=df, fwd_slot=res_slot,
+                        fwd_count=dc)
+    ctx.submit_ring(ring, 5, 7)      # slots 5..8, 0..2
+    ctx.submit_ring(ring, 3, 2)      # slots 3, 4
+    ctx.sync()
+    fwo, rto = oracle_tables(rules, routes)
+    res_all = dr.download(cg.RESULT_DT, res_slot * P)
+    fwd_all = df.download(np.uint32, res_slot * P)
+    cnt = dc.download(np.uint32, P)
+    for s in range(P):
+        ro, fo, _ = orc.process(pk[s * n * 64:(s + 1) * n * 64], n, stages=S | F | L, fw=fwo, route=rto)
+        rg = res_all[s * res_slot: s * res_slot + n]
+        fg = fwd_all[s * res_slot: s * res_slot + cnt[s]]
+        assert_parity(rg, fg, ro, fo)
+
+
+def test_ring_large_launch_many_batches(gpu_ctx_factory):
+    """One launch over 128 ring slots (more than the 32 kernel-argument
+    descriptors): tickets and look-back of every batch stay separate."""
+    rules = fw1k()
+    ctx = setup_ctx(gpu_ctx_factory, rules, n_streams=1)
+    n, P = 8192, 40
+    pk = cg.gen_trace(0x5EED0A00, n * P, rules)
+    dp = ctx.alloc(pk.nbytes)
+    dp.upload(pk)
+    dr = ctx.alloc(n * P * 8)
+    df = ctx.alloc(n * P * 4)
+    dc = ctx.alloc(P * 4)
+    ring = cg.make_ring(dp, P, n, dr, n * 64, fwd_idx=df, fwd_count=dc)
+    for rep in range(3):
+        ctx.submit_ring(ring, (rep * 7) % P, 128)   # each slot processed 3-4 times per launch
+    ctx.sync()
+    fwo, _ = oracle_tables(rules)
+    ro, fo, _ = orc.process(pk, n * P, stages=S | F, fw=fwo)
+    res = dr.download(cg.RESULT_DT, n * P)
+    assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
+    cnt = dc.download(np.uint32, P)
+    fwd = df.download(np.uint32, n * P)
+    got = np.concatenate([fwd[s * n: s * n + cnt[s]] + s * n for s in range(P)])
+    assert np.array_equal(got, fo)

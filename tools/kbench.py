@@ -75,13 +75,24 @@ def main():
     for dbg in (1, 2, 3, 7):
         variants[f"nc_dbg{dbg}"] = (S | F, 0, 16, False, (("COP_DBG", str(dbg)),))
     variants["c_dbg1"] = (S | F, 0, 16, True, (("COP_DBG", "1"),))
+    for Lr in (16, 32, 64, 100):
+        for ns in (1, 2):
+            variants[f"ring_L{Lr}_s{ns}"] = (S | F, 0, Lr, True, (("COP_STREAMS", str(ns)),), "ring")
+    variants["ring_lpm_L64_s1"] = (S | F | L, 0, 64, True, (("COP_STREAMS", "1"),), "ring")
     names = [v for v in args.variants.split(",") if v] or list(variants)
     res = {n: [] for n in names}
     for r in range(args.rounds):
         for n in names:
             stages, flags, Lb, compact, *env = variants[n]
             ctx = ctx_for(stages, flags, env[0] if env else ())
-            def sub(i0):
+            is_ring = len(env) > 1 and env[1] == "ring"
+            ring = cg.make_ring(d_pk, P, B, d_res, B * 64, fwd_idx=d_fwd if compact else None,
+                                fwd_count=d_cnt if compact else None)
+
+            def sub_ring(i0):
+                ctx.submit_ring(ring, i0 % P, Lb)
+
+            def sub_desc(i0):
                 bl = []
                 for j in range(Lb):
                     i = (i0 + j) % P
@@ -89,6 +100,7 @@ def main():
                                             fwd_idx=(d_fwd.addr + i * B * 4) if compact else None,
                                             fwd_count=(d_cnt.addr + i * 4) if compact else None))
                 ctx.submit(bl)
+            sub = sub_ring if is_ring else sub_desc
             for w in range(3):
                 sub(w * Lb)
             ctx.sync()
