@@ -79,6 +79,12 @@ def main():
         for ns in (1, 2):
             variants[f"ring_L{Lr}_s{ns}"] = (S | F, 0, Lr, True, (("COP_STREAMS", str(ns)),), "ring")
     variants["ring_lpm_L64_s1"] = (S | F | L, 0, 64, True, (("COP_STREAMS", "1"),), "ring")
+    variants["ring_L96_s1"] = (S | F, 0, 96, True, (("COP_STREAMS", "1"),), "ring")
+    variants["ring_L96_s1_static"] = (S | F, 0, 96, True, (("COP_STREAMS", "1"), ("COP_DBG", "2")), "ring")
+    variants["ring_L96_s1_nocompact"] = (S | F, 0, 96, False, (("COP_STREAMS", "1"),), "ring")
+    variants["ring_L96_s1_p4"] = (S | F, 0, 96, True, (("COP_STREAMS", "1"), ("COP_PPT", "4")), "ring")
+    variants["ring_lpm_L96_s1"] = (S | F | L, 0, 96, True, (("COP_STREAMS", "1"),), "ring")
+    variants["ring_lpm_L96_s1_static"] = (S | F | L, 0, 96, True, (("COP_STREAMS", "1"), ("COP_DBG", "2")), "ring")
     names = [v for v in args.variants.split(",") if v] or list(variants)
     res = {n: [] for n in names}
     for r in range(args.rounds):

@@ -39,6 +39,49 @@ __global__ __launch_bounds__(256) void kA(const uint8_t *__restrict__ pk, uint32
     }
 }
 
+// kA with grid-interleaved steps: at step k every workgroup reads inside one
+// contiguous window (packet = k*grid*256 + blockIdx*256 + tid)
+template <int PPT>
+__global__ __launch_bounds__(256) void kE(const uint8_t *__restrict__ pk, uint32_t *__restrict__ out, uint32_t n) {
+    uint32_t w3[PPT], w6[PPT], w7[PPT], w8[PPT];
+    const uint32_t span = gridDim.x * 256;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        uint32_t i = min(k * span + blockIdx.x * 256 + threadIdx.x, n - 1);
+        const uint8_t *p = pk + (size_t)i * 64;
+        w3[k] = *(const uint32_t *)(p + 12);
+        uint2 v = *(const uint2 *)(p + 24);
+        w6[k] = v.x; w7[k] = v.y;
+        w8[k] = *(const uint32_t *)(p + 32);
+    }
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        uint32_t i = k * span + blockIdx.x * 256 + threadIdx.x;
+        if (i < n) out[i] = mixw(w3[k], w6[k], w7[k], w8[k]);
+    }
+}
+
+// kA with 8-byte result records written per packet (the pipeline's write mix)
+template <int PPT>
+__global__ __launch_bounds__(256) void kF(const uint8_t *__restrict__ pk, uint2 *__restrict__ out, uint32_t n) {
+    const uint32_t base = blockIdx.x * 256 * PPT;
+    uint32_t w3[PPT], w6[PPT], w7[PPT], w8[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        uint32_t i = min(base + k * 256 + threadIdx.x, n - 1);
+        const uint8_t *p = pk + (size_t)i * 64;
+        w3[k] = *(const uint32_t *)(p + 12);
+        uint2 v = *(const uint2 *)(p + 24);
+        w6[k] = v.x; w7[k] = v.y;
+        w8[k] = *(const uint32_t *)(p + 32);
+    }
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        uint32_t i = base + k * 256 + threadIdx.x;
+        if (i < n) out[i] = make_uint2(mixw(w3[k], w6[k], w7[k], w8[k]), w3[k]);
+    }
+}
+
 template <int PPT>
 __global__ __launch_bounds__(256) void kB(const uint8_t *__restrict__ pk, uint32_t *__restrict__ out, uint32_t n) {
     // wave w of the block handles packets [base + w*64*PPT + s*64, +64) per step s;
@@ -120,7 +163,7 @@ int main() {
     const uint32_t n = 5u << 20;              // 5 Mi packets = 320 MiB
     uint8_t *pk; uint32_t *out;
     CHK(hipMalloc(&pk, (size_t)n * 64));
-    CHK(hipMalloc(&out, (size_t)n * 4 + (1 << 24)));
+    CHK(hipMalloc(&out, (size_t)n * 8 + (1 << 24)));
     CHK(hipMemset(pk, 0x5A, (size_t)n * 64));
     hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
     auto timeit = [&](const char *name, auto launch, double bytes) {
@@ -137,6 +180,9 @@ int main() {
     timeit("A strided ppt4", [&] { hipLaunchKernelGGL(kA<4>, dim3((n + 1023) / 1024), dim3(256), 0, 0, pk, out, n); }, alg);
     timeit("A strided ppt8", [&] { hipLaunchKernelGGL(kA<8>, dim3((n + 2047) / 2048), dim3(256), 0, 0, pk, out, n); }, alg);
     timeit("A strided ppt16", [&] { hipLaunchKernelGGL(kA<16>, dim3((n + 4095) / 4096), dim3(256), 0, 0, pk, out, n); }, alg);
+    timeit("E interleaved ppt8", [&] { hipLaunchKernelGGL(kE<8>, dim3((n + 2047) / 2048), dim3(256), 0, 0, pk, out, n); }, alg);
+    timeit("E interleaved ppt4", [&] { hipLaunchKernelGGL(kE<4>, dim3((n + 1023) / 1024), dim3(256), 0, 0, pk, out, n); }, alg);
+    timeit("F strided+8B rec ppt8", [&] { hipLaunchKernelGGL(kF<8>, dim3((n + 2047) / 2048), dim3(256), 0, 0, pk, (uint2 *)out, n); }, 72.0 * n);
     timeit("B coalesced+lds ppt4", [&] { hipLaunchKernelGGL(kB<4>, dim3((n + 1023) / 1024), dim3(256), 0, 0, pk, out, n); }, alg);
     timeit("B coalesced+lds ppt8", [&] { hipLaunchKernelGGL(kB<8>, dim3((n + 2047) / 2048), dim3(256), 0, 0, pk, out, n); }, alg);
     timeit("C glds ppt4", [&] { hipLaunchKernelGGL(kC<4>, dim3((n + 1023) / 1024), dim3(256), 32768, 0, pk, out, n); }, alg);

@@ -19,21 +19,26 @@ S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
 PH = ["ticket+stage", "loads+P", "lookups", "store", "compact", "tail"]
 
 
-def run(stages, Lb, compact, label):
+def run(stages, Lb, compact, label, ring=False):
     fw = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
     routes = cg.gen_rules(0x5EED2004, 100000, cg.GEN_ROUTES, 0)
     ctx = cg.Context(stages=stages)
     ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
     ctx.set_route_lpm(cg.LpmTable(routes, 1 << 20, 1 << 16, False))
     B = 65536
-    P = 64
+    P = 100 if ring else 64
     dp = ctx.alloc(P * B * 64)
     for i in range(0, P, 16):
-        dp.upload(cg.gen_trace(0x5EED0002 + i, 16 * B, fw, routes), i * B * 64)
+        k = min(16, P - i)
+        dp.upload(cg.gen_trace(0x5EED0002 + i, k * B, fw, routes), i * B * 64)
     dr = ctx.alloc(P * B * 8)
     df = ctx.alloc(P * B * 4)
     dc = ctx.alloc(P * 4)
+    rg = cg.make_ring(dp, P, B, dr, B * 64, fwd_idx=df if compact else None, fwd_count=dc if compact else None)
     for it in range(6):
+        if ring:
+            ctx.submit_ring(rg, 0, Lb)
+            continue
         bl = []
         for j in range(Lb):
             i = (it * Lb + j) % P
@@ -65,10 +70,19 @@ def run(stages, Lb, compact, label):
             break
         d = (st[:, b] - st[:, a]) * 10 / 1000
         print(f"   {name:14s} median {np.median(d):6.2f}  p90 {np.percentile(d, 90):6.2f} us")
+    # workgroups in flight over the launch (5 us buckets)
+    t_end = (st[:, 6] - t0) * 10 / 1000
+    edges = np.arange(0, t_end.max() + 5, 5)
+    act = [int(((starts < e + 5) & (t_end > e)).sum()) for e in edges]
+    print("   active WGs per 5us:", act)
     ctx.close()
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "ring":
+        run(S | F, 96, True, "fw ring L96 compact", ring=True)
+        run(S | F | L, 96, True, "fw+lpm ring L96 compact", ring=True)
+        sys.exit(0)
     run(S | F, 16, True, "fw L16 compact")
     run(S | F, 16, False, "fw L16 no-compact")
     run(S | F, 1, True, "fw L1 compact")
