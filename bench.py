@@ -45,7 +45,9 @@ WORKLOADS = {
     "fw_lpm": dict(cid=4, stages=S | F | L, fw=1000, routes=100000, imix=False, batch=65536,
                    desc="firewall + LPM 100k, 64B pkts, batch 64k per GPU (BASELINE configs[3])"),
     "fw_lpm_1m": dict(cid=5, stages=S | F | L, fw=1000000, routes=1000000, imix=False, batch=262144,
-                      desc="1M ACL rules + 1M LPM prefixes, 64B, batch 256k per GPU (BASELINE configs[4])"),
+                      rule_counters=True,
+                      desc="1M ACL rules + 1M LPM prefixes, 64B, batch 256k per GPU, per-rule hit "
+                           "counters all-reduced over RCCL once per timed region (BASELINE configs[4])"),
 }
 
 
@@ -64,6 +66,8 @@ def main():
     ap.add_argument("--pool-mib", type=int, default=400, help="distinct input bytes per GPU")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-rule-counters", action="store_true", help="ablation: config 5 without per-rule counters")
+    ap.add_argument("--stages", type=int, default=0, help="ablation: override the workload's stage mask")
     args = ap.parse_args()
 
     rank, world, local = copdist.env()
@@ -84,8 +88,16 @@ def main():
         fw_tab = cg.LpmTable(fw_rules, 1024, 24, True)                  # lpm_setup's own limits
     else:
         fw_tab = cg.LpmTable(fw_rules, W["fw"], 1 << 20, False)
-    ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32, n_streams=args.streams)
+    rc_on = bool(W.get("rule_counters")) and not args.no_rule_counters
+    if args.stages:
+        W = dict(W, stages=args.stages)
+    ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32, n_streams=args.streams,
+                     flags=cg.CFG_RULE_COUNTERS if rc_on else 0)
     ctx.set_fw_table(fw_tab)
+    if rc_on:
+        # RCCL communicator over the GPUs of the job (xGMI); id from rank 0 over gloo
+        uid = group.broadcast_bytes(cg.coll_unique_id() if rank == 0 else None)
+        ctx.coll_init(uid, rank, world)
     if routes is not None:
         ctx.set_route_lpm(cg.LpmTable(routes, max(W["routes"], 1), 1 << 20, False))
     log(f"[rank {rank}] tables ready in {time.time() - t0:.1f}s on device {dev}")
@@ -138,6 +150,9 @@ def main():
     ctx.sync()
     t0 = time.perf_counter()
     run_steps(args.warmup, args.steps)
+    if rc_on:
+        # one reporting interval: sum counters + per-rule hits over all GPUs
+        red_tot, _ = ctx.coll_reduce_counters(reset=True, with_rules=False)
     ctx.sync()
     t1 = time.perf_counter()
     group.barrier()
@@ -145,6 +160,19 @@ def main():
     total_pkts = world * args.steps * B
     value = total_pkts / elapsed / 1e6
     log(f"[rank {rank}] timed {args.steps} steps in {elapsed * 1e3:.2f} ms -> {value:.1f} Mpkt/s (all ranks)")
+
+    reduce_info = None
+    if rc_on:
+        # the reduction alone (counters are zero now: same bytes, same cost)
+        group.barrier()
+        r0 = time.perf_counter()
+        ctx.coll_reduce_counters(reset=False, with_rules=False)
+        r_ms = (time.perf_counter() - r0) * 1e3
+        n_rules = len(ctx.rule_counters())
+        reduce_info = {"rccl_allreduce_u64_words": 1024 + n_rules, "ms": round(group.max(r_ms), 3),
+                       "pkts_reduced": int(red_tot["rx"]), "expected_pkts": world * (args.warmup + args.steps) * B}
+        assert red_tot["rx"] == world * (args.warmup + args.steps) * B, (red_tot, world, args.steps)
+        log(f"[rank {rank}] rccl counter all-reduce of {1024 + n_rules} u64: {r_ms:.3f} ms")
 
     # ---- kernel duration per launch (HIP events on the context stream) ----
     ctx.counters(reset=True)
@@ -196,6 +224,7 @@ def main():
             "stages": W["stages"],
             "parallelism": f"independent per-GPU contexts x{world} (no data-path collective)",
             "pool_batches": int(P),
+            "rule_counters": rc_on,
         },
         "roofline": {
             "bound": "hbm",
@@ -211,6 +240,8 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if reduce_info:
+        out["counter_reduce"] = reduce_info
 
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

@@ -1,12 +1,15 @@
 """One process per GPU for the coprocessor pipeline.
 
 Packet batches shard with no data-path exchange: every rank owns one GPU,
-one context, its own packet stream and a replica of the tables. The only
-collectives are control-plane ones, over gloo on host tensors:
+one context, its own packet stream and a replica of the tables. Control-
+plane collectives run over gloo on host tensors:
   - a barrier around the timed region and the max of elapsed times,
-  - sums of u64 counter arrays (cop_counters, per-rule hits) at a reporting
-    interval — the analogue of the reference's print_stats every
-    PRINT_DELAY = 2 s (switch.h:23, switch.c:33-90).
+  - the RCCL unique id broadcast from rank 0.
+The one device collective is the counter reduction of BASELINE configs[4]:
+the per-GPU counter shards + per-rule hit counters are summed with an RCCL
+all-reduce over xGMI (cop_coll_reduce_counters) at a reporting interval —
+the analogue of the reference's print_stats every PRINT_DELAY = 2 s
+(switch.h:23, switch.c:33-90). sum_u64 is the gloo fallback of that sum.
 """
 from __future__ import annotations
 
@@ -64,6 +67,14 @@ class Group:
         t = torch.from_numpy(a.view(np.int64).copy())
         self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM)
         return t.numpy().view(np.uint64)
+
+    def broadcast_bytes(self, b: bytes | None, root: int = 0) -> bytes:
+        """Rank `root` passes the bytes, the others None; all get them back."""
+        if not self._dist:
+            return b
+        obj = [b]
+        self._dist.broadcast_object_list(obj, src=root)
+        return obj[0]
 
     def close(self):
         if self._dist and self._dist.is_initialized():

@@ -22,7 +22,7 @@ STAGE_PARSE, STAGE_FW, STAGE_LPM = 0x1, 0x2, 0x4
 FORWARD, DROP_FW, DROP_PARSE, DROP_NOT_IPV4, DROP_NO_PORT = 0, 1, 2, 3, 4
 FLAG_ROUTE_HIT, FLAG_FW_HIT = 0x1, 0x2
 LPM_STOP_AT_FIRST_ERROR = 0x1
-CFG_FW_FORCE_DIR24, CFG_LPM_FORCE_DIR24, CFG_NO_COMPACT = 0x1, 0x2, 0x4
+CFG_FW_FORCE_DIR24, CFG_LPM_FORCE_DIR24, CFG_NO_COMPACT, CFG_RULE_COUNTERS = 0x1, 0x2, 0x4, 0x8
 GEN_FW, GEN_ROUTES = 0, 1
 UNKNOWN_PORT = 0xFFFF
 
@@ -89,6 +89,7 @@ SIGNATURES = {
     "cop_lpm_export_dir24": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32]),
     "cop_lpm_export_intervals": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32]),
     "cop_lpm_export_rules": (c_int, [c_void_p, c_void_p, c_uint32]),
+    "cop_lpm_lookup_rules": (c_int, [c_void_p, c_void_p, c_uint32, c_void_p]),
     "cop_rules_load_json": (c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
     "cop_rules_free": (None, [c_void_p]),
     "cop_rules_write_json": (c_int, [c_char_p, c_void_p, c_uint32]),
@@ -110,6 +111,11 @@ SIGNATURES = {
     "cop_process_host_stream": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
     "cop_counters_read": (c_int, [c_void_p, c_void_p, c_int]),
     "cop_counters_device_ptr": (c_void_p, [c_void_p]),
+    "cop_rule_counters_read": (c_int, [c_void_p, c_void_p, c_uint32, c_int]),
+    "cop_rule_counters_device_ptr": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint32)]),
+    "cop_coll_unique_id": (c_int, [c_void_p]),
+    "cop_coll_init": (c_int, [c_void_p, c_void_p, c_int, c_int]),
+    "cop_coll_reduce_counters": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_int]),
     "cop_dev_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
     "cop_dev_free": (c_int, [c_void_p, c_void_p]),
     "cop_host_alloc_pinned": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
@@ -268,6 +274,13 @@ class LpmTable:
         _check(lib().cop_lpm_export_rules(self.handle, _ptr(out), n))
         return out
 
+    def lookup_rules(self, ips: np.ndarray) -> np.ndarray:
+        """Matching rule id per address (-1 on a miss), host-side."""
+        ips = np.ascontiguousarray(ips, dtype=np.uint32)
+        out = np.zeros(len(ips), dtype=np.int32)
+        _check(lib().cop_lpm_lookup_rules(self.handle, _ptr(ips), len(ips), _ptr(out)))
+        return out
+
     def intervals(self):
         m = _check(lib().cop_lpm_export_intervals(self.handle, None, None, 1 << 31))
         s = np.zeros(m, dtype=np.uint32)
@@ -322,6 +335,16 @@ class DeviceBuffer:
                 self.free()
         except Exception:
             pass
+
+
+COLL_ID_BYTES = 128
+
+
+def coll_unique_id() -> bytes:
+    """RCCL unique id (rank 0 creates it; the caller distributes it)."""
+    buf = (c_uint8 * COLL_ID_BYTES)()
+    _check(lib().cop_coll_unique_id(buf), what="cop_coll_unique_id")
+    return bytes(buf)
 
 
 def device_count() -> int:
@@ -404,6 +427,28 @@ class Context:
 
     def counters_device_ptr(self) -> int:
         return lib().cop_counters_device_ptr(self.handle)
+
+    def rule_counters(self, reset=False) -> np.ndarray:
+        """Per-rule FW hit counters (CFG_RULE_COUNTERS), indexed by rule id."""
+        n = _check(lib().cop_rule_counters_read(self.handle, None, 0, 0), self, "rule_counters")
+        out = np.zeros(n, dtype=np.uint64)
+        _check(lib().cop_rule_counters_read(self.handle, _ptr(out), n, 1 if reset else 0), self, "rule_counters")
+        return out
+
+    def coll_init(self, uid: bytes, rank: int, nranks: int):
+        buf = (c_uint8 * COLL_ID_BYTES).from_buffer_copy(uid)
+        _check(lib().cop_coll_init(self.handle, buf, rank, nranks), self, "coll_init")
+
+    def coll_reduce_counters(self, reset=False, with_rules=True):
+        """RCCL all-reduce of counters (+ per-rule counters) over the ranks."""
+        c = np.zeros(16, dtype=np.uint64)
+        n = 0
+        if with_rules and (self.cfg.flags & CFG_RULE_COUNTERS):
+            n = _check(lib().cop_rule_counters_read(self.handle, None, 0, 0), self, "rule_counters")
+        hits = np.zeros(max(n, 1), dtype=np.uint64)
+        _check(lib().cop_coll_reduce_counters(self.handle, _ptr(c), _ptr(hits), n, 1 if reset else 0), self,
+               "coll_reduce_counters")
+        return {k: int(c[i]) for i, k in enumerate(COUNTER_NAMES)}, hits[:n]
 
     def process_host(self, pkts: np.ndarray, n: int, stride: int = 64):
         """End-to-end: host packet memory -> pinned gather -> H2D -> kernel -> D2H."""

@@ -35,8 +35,30 @@ struct cop_lpm_table {
     uint32_t *iv_val;      /* internal value incl. depth */
     uint32_t  tbl8_used;   /* DPDK-semantics tbl8 groups (acceptance) */
     uint32_t  n_ext;       /* /24 blocks that need a tbl8 group in our image */
+    /* the same function keyed by matching rule id (index into rule_*;
+     * COP_NO_RULE on a miss): the firewall's device image form */
+    uint32_t  n_rv;
+    uint32_t *rv_start;
+    uint32_t *rv_rule;
+    uint32_t  n_ext_rule;
     cop_lpm_report report;
 };
+
+#define COP_NO_RULE 0xFFFFFFFFu
+
+/* Device image forms. NH: entry = next_hop | VALID (the route stage).
+ * RULE: entry = rule_id | VALID | DROP (bit 26: the rule's next hop, i.e.
+ * its firewall action, is non-zero) — the firewall stage, which needs the
+ * verdict and the matching rule (per-rule hit counters), not the action. */
+enum { COP_FORM_NH = 0, COP_FORM_RULE = 1 };
+#define COP_RV_DROP 0x04000000u
+
+/* Merged (start, device entry) intervals of a form; arrays are malloc-ed. */
+uint32_t cop_lpm_form_intervals(const cop_lpm_table *t, int form, uint32_t **starts, uint32_t **entries);
+/* /24 blocks with an interior boundary in a form's image (tbl8 groups). */
+uint32_t cop_lpm_form_n_ext(const cop_lpm_table *t, int form);
+/* Paint a form's DIR-24-8 image (tbl24: 1<<24, tbl8: n_ext(form) * 256). */
+void cop_lpm_form_fill_dir24(const cop_lpm_table *t, int form, uint32_t *tbl24, uint32_t *tbl8);
 
 /* Flatten (hit,nh) only: merged interval arrays for the LDS search form.
  * Returns the count; the starts and vals arrays are malloc-ed. */

@@ -84,6 +84,7 @@ struct CopKParams {
     uint32_t zero_lines;               // its dirty lines
     unsigned long long *look;
     unsigned long long *counters;
+    unsigned long long *rule_hits;     // per-rule FW hit counters or nullptr
     uint32_t *err;
     unsigned long long *stamps;   // diagnostic phase stamps (dbg bit 8)
 };

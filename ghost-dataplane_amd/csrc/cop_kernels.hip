@@ -12,7 +12,10 @@
 //
 // Data layout (HBM): packets at 16-byte aligned starts (64-byte slots or an
 // IMIX slab + u32 offsets). Tables: the vport routing table as a two-level
-// image (256-entry top + 256-entry u16 leaves); LPM tables either as a
+// image (256-entry top + 256-entry u16 leaves); the firewall table keyed by
+// matching rule id (entry = rule | hit<<24 | (action != 0)<<26, so the
+// verdict and the per-rule hit counter come from one probe) and the route
+// table keyed by next hop; LPM tables either as a
 // flattened interval array (binary search in LDS) or as a DPDK-layout
 // DIR-24-8 image (tbl24 64 MiB + tbl8 groups, HBM / Infinity Cache). Small
 // tables are staged into LDS by LDS-DMA at workgroup start, overlapped with
@@ -272,14 +275,25 @@ __global__ __launch_bounds__(BLOCK) void cop_pipeline(const CopKParams p)
                 verdict[k] = COPK_DROP_NOT_IPV4;
                 c_notv4 += valid[k];
             } else {
+                // rule-id image: bit 24 hit, bit 26 = the matching rule's
+                // action is non-zero (switch(rule) at firewall.c:201-210)
                 flags[k] |= (fwe[k] >> 24) & 1u ? COPK_FLAG_FW_HIT : 0u;
-                verdict[k] = (fwe[k] & 0x00FFFFFFu) ? COPK_DROP_FW : COPK_FORWARD;
+                verdict[k] = (fwe[k] >> 26) & 1u ? COPK_DROP_FW : COPK_FORWARD;
             }
         }
         if (LPM != COPK_TBL_OFF) {
             flags[k] |= (lpe[k] >> 24) & 1u ? COPK_FLAG_ROUTE_HIT : 0u;
             rnh[k] = lpe[k] & 0x00FFFFFFu;
         }
+    }
+    if (FW != COPK_TBL_OFF && p.rule_hits) {
+        // per-rule hit counters: one relaxed device-scope u64 add per hit
+        // (no return value: fire-and-forget atomics at the L2/fabric)
+#pragma unroll
+        for (int k = 0; k < PPT; k++)
+            if (valid[k] && (flags[k] & COPK_FLAG_FW_HIT))
+                __hip_atomic_fetch_add(&p.rule_hits[fwe[k] & 0x00FFFFFFu], 1ull, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
     }
     if (p.dbg & 8u) {
         uint32_t x = 0;

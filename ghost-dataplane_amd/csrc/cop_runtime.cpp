@@ -9,6 +9,7 @@
 // coprocessor thread or per GPU, no globals.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
 #include <errno.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -20,6 +21,7 @@
 #include "cop_gpu.h"
 #include "cop_internal.h"
 #include "cop_kernels.h"
+#include <rccl/rccl.h>   // types only: librccl is dlopen-ed on first use
 
 namespace {
 
@@ -80,7 +82,11 @@ struct cop_ctx {
     DevLpm fw, lpm;
 
     uint32_t look_cap = 0;
-    unsigned long long *counters = nullptr;     // COPK_COUNTER_SHARDS x 16 u64
+    unsigned long long *counters = nullptr;     // COPK_COUNTER_SHARDS x 16 u64 [+ per-rule u64]
+    uint32_t n_rule_ctr = 0;                    // per-rule words after the shards
+    unsigned long long *ctr_sum = nullptr;      // RCCL all-reduce destination
+    size_t ctr_sum_words = 0;
+    ncclComm_t comm = nullptr;
     uint32_t *h_err = nullptr;                  // host-mapped
     uint32_t *d_err = nullptr;
 
@@ -157,6 +163,8 @@ static void free_lpm(DevLpm &t)
     t = DevLpm();
 }
 
+static void coll_destroy(cop_ctx *c);
+
 void cop_destroy(cop_ctx *c)
 {
     if (!c) return;
@@ -169,6 +177,8 @@ void cop_destroy(cop_ctx *c)
     if (c->rt_leaf) (void)hipFree(c->rt_leaf);
     if (c->stamps) (void)hipFree(c->stamps);
     if (c->counters) (void)hipFree(c->counters);
+    if (c->ctr_sum) (void)hipFree(c->ctr_sum);
+    coll_destroy(c);
     if (c->h_err) (void)hipHostFree(c->h_err);
     if (c->t0) (void)hipEventDestroy(c->t0);
     if (c->t1) (void)hipEventDestroy(c->t1);
@@ -355,13 +365,15 @@ static int sync_lanes(cop_ctx *c)
     return 0;
 }
 
-static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt)
+// form: COP_FORM_RULE for the firewall (entries carry the matching rule id
+// and the drop bit), COP_FORM_NH for the route stage (entries carry nh)
+static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt, int form)
 {
     if (int rc = sync_lanes(c)) return rc;
     free_lpm(t);
     // interval form for LDS
     uint32_t *s = nullptr, *v = nullptr;
-    uint32_t m = cop_lpm_merged_intervals(tab, &s, &v);
+    uint32_t m = cop_lpm_form_intervals(tab, form, &s, &v);
     if (!s) return set_err(c, -ENOMEM, "interval export failed");
     if (want_ivt && m <= IVT_MAX) {
         // Eytzinger image: tree[1..M-1] = sorted starts s[1..M-1] in BFS
@@ -397,28 +409,51 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
     free(s);
     free(v);
     // DIR-24-8 image (always: FORCE_DIR24 and the large-table path)
+    const uint32_t n_ext = cop_lpm_form_n_ext(tab, form);
     std::vector<uint32_t> h24((size_t)1 << 24);
-    std::vector<uint32_t> h8((size_t)(tab->n_ext ? tab->n_ext : 1) * 256);
-    cop_lpm_fill_dir24(tab, h24.data(), h8.data());
+    std::vector<uint32_t> h8((size_t)(n_ext ? n_ext : 1) * 256);
+    cop_lpm_form_fill_dir24(tab, form, h24.data(), h8.data());
     HIPCHK(c, hipMalloc(&t.tbl24, h24.size() * 4));
     HIPCHK(c, hipMalloc(&t.tbl8, h8.size() * 4));
     HIPCHK(c, hipMemcpy(t.tbl24, h24.data(), h24.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(t.tbl8, h8.data(), h8.size() * 4, hipMemcpyHostToDevice));
-    t.n_ext = tab->n_ext;
+    t.n_ext = n_ext;
     t.loaded = true;
+    return 0;
+}
+
+// counter buffer = shards (COPK_COUNTER_SHARDS x 16) followed by n_rules
+// per-rule words; the shard words are carried over, the rule words zeroed
+static int resize_counters(cop_ctx *c, uint32_t n_rules)
+{
+    const size_t shard_words = (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS;
+    unsigned long long *nb = nullptr;
+    HIPCHK(c, hipMalloc(&nb, (shard_words + n_rules) * 8));
+    hipError_t e = hipMemcpy(nb, c->counters, shard_words * 8, hipMemcpyDeviceToDevice);
+    if (e == hipSuccess && n_rules) e = hipMemset(nb + shard_words, 0, (size_t)n_rules * 8);
+    if (e != hipSuccess) {
+        (void)hipFree(nb);
+        return set_err(c, -EIO, "counter resize: %s", hipGetErrorString(e));
+    }
+    (void)hipFree(c->counters);
+    c->counters = nb;
+    c->n_rule_ctr = n_rules;
     return 0;
 }
 
 int cop_set_fw_table(cop_ctx *c, const cop_lpm_table *t)
 {
     if (!c || !t) return -EINVAL;
-    return upload_lpm(c, c->fw, t, !(c->cfg.flags & COP_CFG_FW_FORCE_DIR24));
+    if (t->n_rules > COP_LPM_NH_MASK) return set_err(c, -EINVAL, "rule ids exceed 24 bits");
+    int rc = upload_lpm(c, c->fw, t, !(c->cfg.flags & COP_CFG_FW_FORCE_DIR24), COP_FORM_RULE);
+    if (!rc && (c->cfg.flags & COP_CFG_RULE_COUNTERS)) rc = resize_counters(c, t->n_rules);
+    return rc;
 }
 
 int cop_set_route_lpm(cop_ctx *c, const cop_lpm_table *t)
 {
     if (!c || !t) return -EINVAL;
-    return upload_lpm(c, c->lpm, t, !(c->cfg.flags & COP_CFG_LPM_FORCE_DIR24));
+    return upload_lpm(c, c->lpm, t, !(c->cfg.flags & COP_CFG_LPM_FORCE_DIR24), COP_FORM_NH);
 }
 
 int cop_load_fw_rules_file(cop_ctx *c, const char *path, const cop_lpm_config *cfg,
@@ -538,6 +573,9 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, int ppt, uin
     p.zero_lines = L.dirty[q ^ 1];
     p.look = L.look;
     p.counters = c->counters;
+    p.rule_hits = (fw_mode != COPK_TBL_OFF && c->n_rule_ctr)
+                      ? c->counters + (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS
+                      : nullptr;
     p.err = c->d_err;
     p.stamps = c->stamps;
     if ((c->dbg & 8u) && p.ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
@@ -810,6 +848,124 @@ int cop_counters_read(cop_ctx *c, cop_counters *out, int reset)
 }
 
 void *cop_counters_device_ptr(cop_ctx *c) { return c ? (void *)c->counters : nullptr; }
+
+int cop_rule_counters_read(cop_ctx *c, uint64_t *out, uint32_t cap, int reset)
+{
+    if (!c || (cap && !out)) return -EINVAL;
+    if (!(c->cfg.flags & COP_CFG_RULE_COUNTERS)) return set_err(c, -EINVAL, "rule counters not enabled");
+    if (int rc = sync_lanes(c)) return rc;
+    unsigned long long *d = c->counters + (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS;
+    const uint32_t k = cap < c->n_rule_ctr ? cap : c->n_rule_ctr;
+    if (k) HIPCHK(c, hipMemcpy(out, d, (size_t)k * 8, hipMemcpyDeviceToHost));
+    if (reset && c->n_rule_ctr) HIPCHK(c, hipMemset(d, 0, (size_t)c->n_rule_ctr * 8));
+    return (int)c->n_rule_ctr;
+}
+
+int cop_rule_counters_device_ptr(cop_ctx *c, void **dptr, uint32_t *n_rules)
+{
+    if (!c || !dptr) return -EINVAL;
+    if (!(c->cfg.flags & COP_CFG_RULE_COUNTERS)) return set_err(c, -EINVAL, "rule counters not enabled");
+    *dptr = c->counters + (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS;
+    if (n_rules) *n_rules = c->n_rule_ctr;
+    return 0;
+}
+
+// ---- RCCL (xGMI) counter reduction ----------------------------------------
+// librccl is opened lazily so that the library (and every single-GPU path)
+// works on hosts without it.
+namespace {
+struct Rccl {
+    bool tried = false, ok = false;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+};
+Rccl g_rccl;
+}  // namespace
+
+static bool rccl_load()
+{
+    Rccl &r = g_rccl;
+    if (r.tried) return r.ok;
+    r.tried = true;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return false;
+    r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
+    r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    r.ok = r.get_unique_id && r.comm_init_rank && r.all_reduce && r.comm_destroy && r.error_string;
+    return r.ok;
+}
+
+static void coll_destroy(cop_ctx *c)
+{
+    if (c->comm && g_rccl.ok) (void)g_rccl.comm_destroy(c->comm);
+    c->comm = nullptr;
+}
+
+int cop_coll_unique_id(uint8_t id[COP_COLL_ID_BYTES])
+{
+    if (!id) return -EINVAL;
+    if (!rccl_load()) return -ENOSYS;
+    ncclUniqueId u;
+    if (g_rccl.get_unique_id(&u) != ncclSuccess) return -EIO;
+    memcpy(id, u.internal, COP_COLL_ID_BYTES);
+    return 0;
+}
+
+int cop_coll_init(cop_ctx *c, const uint8_t id[COP_COLL_ID_BYTES], int rank, int nranks)
+{
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return -EINVAL;
+    if (!rccl_load()) return set_err(c, -ENOSYS, "librccl not available");
+    HIPCHK(c, hipSetDevice(c->device));
+    coll_destroy(c);
+    ncclUniqueId u;
+    memcpy(u.internal, id, COP_COLL_ID_BYTES);
+    ncclResult_t r = g_rccl.comm_init_rank(&c->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        c->comm = nullptr;
+        return set_err(c, -EIO, "ncclCommInitRank: %s", g_rccl.error_string(r));
+    }
+    return 0;
+}
+
+int cop_coll_reduce_counters(cop_ctx *c, cop_counters *total, uint64_t *rule_hits, uint32_t cap, int reset)
+{
+    if (!c || (cap && !rule_hits)) return -EINVAL;
+    if (!c->comm) return set_err(c, -EINVAL, "cop_coll_init not called");
+    if (int rc = sync_lanes(c)) return rc;
+    const size_t shard_words = (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS;
+    const size_t words = shard_words + c->n_rule_ctr;
+    if (c->ctr_sum_words < words) {
+        if (c->ctr_sum) (void)hipFree(c->ctr_sum);
+        c->ctr_sum = nullptr;
+        c->ctr_sum_words = 0;
+        HIPCHK(c, hipMalloc(&c->ctr_sum, words * 8));
+        c->ctr_sum_words = words;
+    }
+    // ranks hold the same rule table, so the per-rule ranges line up
+    ncclResult_t r = g_rccl.all_reduce(c->counters, c->ctr_sum, words, ncclUint64, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) return set_err(c, -EIO, "ncclAllReduce: %s", g_rccl.error_string(r));
+    if (reset) HIPCHK(c, hipMemsetAsync(c->counters, 0, words * 8, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (total) {
+        std::vector<uint64_t> sh(shard_words);
+        HIPCHK(c, hipMemcpy(sh.data(), c->ctr_sum, shard_words * 8, hipMemcpyDeviceToHost));
+        uint64_t sum[COP_N_COUNTERS] = {0};
+        for (int s = 0; s < COPK_COUNTER_SHARDS; s++)
+            for (int k = 0; k < COP_N_COUNTERS; k++) sum[k] += sh[(size_t)s * COP_N_COUNTERS + k];
+        memcpy(total, sum, sizeof(cop_counters));
+    }
+    const uint32_t k = cap < c->n_rule_ctr ? cap : c->n_rule_ctr;
+    if (k) HIPCHK(c, hipMemcpy(rule_hits, c->ctr_sum + shard_words, (size_t)k * 8, hipMemcpyDeviceToHost));
+    return (int)c->n_rule_ctr;
+}
 
 int cop_dev_alloc(cop_ctx *c, size_t bytes, void **dptr)
 {

@@ -100,6 +100,7 @@ static void umap_commit(umap *m, uint32_t *slot, uint64_t key)
 typedef struct {
     uint32_t ip;
     uint32_t val;
+    uint32_t rule;
     uint8_t  depth;
 } srule;
 
@@ -130,6 +131,20 @@ static void iv_emit(ivbuf *b, uint64_t pos, uint32_t val)
     b->n++;
 }
 
+/* /24 blocks with an interval boundary strictly inside need a tbl8 group */
+static uint32_t count_ext(const uint32_t *start, uint32_t n)
+{
+    uint32_t n_ext = 0, last_blk = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < n; k++) {
+        uint32_t st = start[k];
+        if ((st & 0xFFu) != 0 && (st >> 8) != last_blk) {
+            n_ext++;
+            last_blk = st >> 8;
+        }
+    }
+    return n_ext;
+}
+
 void cop_lpm_free(cop_lpm_table *t)
 {
     if (!t) return;
@@ -138,6 +153,8 @@ void cop_lpm_free(cop_lpm_table *t)
     free(t->rule_nh);
     free(t->iv_start);
     free(t->iv_val);
+    free(t->rv_start);
+    free(t->rv_rule);
     free(t);
 }
 
@@ -241,7 +258,9 @@ int cop_lpm_build(const cop_prefix *rules, uint32_t n, const cop_lpm_config *cfg
     uint32_t ivcap = 2 * t->n_rules + 2;
     t->iv_start = (uint32_t *)malloc((size_t)ivcap * sizeof(uint32_t));
     t->iv_val = (uint32_t *)malloc((size_t)ivcap * sizeof(uint32_t));
-    if (!s || !t->iv_start || !t->iv_val) {
+    t->rv_start = (uint32_t *)malloc((size_t)ivcap * sizeof(uint32_t));
+    t->rv_rule = (uint32_t *)malloc((size_t)ivcap * sizeof(uint32_t));
+    if (!s || !t->iv_start || !t->iv_val || !t->rv_start || !t->rv_rule) {
         free(s);
         cop_lpm_free(t);
         return -ENOMEM;
@@ -250,16 +269,20 @@ int cop_lpm_build(const cop_prefix *rules, uint32_t n, const cop_lpm_config *cfg
         s[i].ip = t->rule_ip[i];
         s[i].depth = t->rule_depth[i];
         s[i].val = t->rule_nh[i] | COP_IV_HIT | ((uint32_t)t->rule_depth[i] << COP_IV_DEPTH_SH);
+        s[i].rule = i;
     }
     qsort(s, t->n_rules, sizeof(srule), srule_cmp);
 
-    ivbuf b = {t->iv_start, t->iv_val, 0};
-    b.start[0] = 0;
+    /* one sweep feeds two interval sets: keyed by value (nh, hit, depth)
+     * and keyed by the matching rule (the firewall's rule-id image) */
+    ivbuf b = {t->iv_start, t->iv_val, 1};
+    ivbuf br = {t->rv_start, t->rv_rule, 1};
+    b.start[0] = br.start[0] = 0;
     b.val[0] = 0;
-    b.n = 1;
+    br.val[0] = COP_NO_RULE;
     struct {
         uint64_t end;
-        uint32_t val;
+        uint32_t val, rule;
     } stk[COP_LPM_MAX_DEPTH + 2];
     int sp = 0;
     for (uint32_t i = 0; i < t->n_rules; i++) {
@@ -268,29 +291,25 @@ int cop_lpm_build(const cop_prefix *rules, uint32_t n, const cop_lpm_config *cfg
         while (sp > 0 && stk[sp - 1].end < st) {
             sp--;
             iv_emit(&b, stk[sp].end + 1, sp ? stk[sp - 1].val : 0u);
+            iv_emit(&br, stk[sp].end + 1, sp ? stk[sp - 1].rule : COP_NO_RULE);
         }
         iv_emit(&b, st, s[i].val);
+        iv_emit(&br, st, s[i].rule);
         stk[sp].end = en;
         stk[sp].val = s[i].val;
+        stk[sp].rule = s[i].rule;
         sp++;
     }
     while (sp > 0) {
         sp--;
         iv_emit(&b, stk[sp].end + 1, sp ? stk[sp - 1].val : 0u);
+        iv_emit(&br, stk[sp].end + 1, sp ? stk[sp - 1].rule : COP_NO_RULE);
     }
     free(s);
     t->n_iv = b.n;
-
-    /* /24 blocks with an interval boundary strictly inside need a tbl8 group */
-    uint32_t n_ext = 0, last_blk = 0xFFFFFFFFu;
-    for (uint32_t k = 0; k < t->n_iv; k++) {
-        uint32_t st = t->iv_start[k];
-        if ((st & 0xFFu) != 0 && (st >> 8) != last_blk) {
-            n_ext++;
-            last_blk = st >> 8;
-        }
-    }
-    t->n_ext = n_ext;
+    t->n_rv = br.n;
+    t->n_ext = count_ext(t->iv_start, t->n_iv);
+    t->n_ext_rule = count_ext(t->rv_start, t->n_rv);
 
     uint32_t *ms = NULL, *mv = NULL;
     rep->n_intervals = cop_lpm_merged_intervals(t, &ms, &mv);
@@ -330,16 +349,24 @@ static inline uint32_t dir_entry(uint32_t ival)
     return ival & ~0x02000000u; /* nh | valid | depth<<26 */
 }
 
-void cop_lpm_fill_dir24(const cop_lpm_table *t, uint32_t *tbl24, uint32_t *tbl8)
+static inline uint32_t rule_entry(const cop_lpm_table *t, uint32_t rule)
+{
+    if (rule == COP_NO_RULE) return 0u;
+    return rule | COP_DIR_VALID | (t->rule_nh[rule] ? COP_RV_DROP : 0u);
+}
+
+/* Paint tbl24/tbl8 from intervals (start[], entry[]) in one pass over the
+ * 2^24 /24 blocks; blocks with an interior boundary get the next tbl8 group. */
+static void fill_dir24(const uint32_t *start, const uint32_t *entry, uint32_t niv, uint32_t *tbl24,
+                       uint32_t *tbl8)
 {
     uint32_t k = 0, g = 0;
-    const uint32_t niv = t->n_iv;
     for (uint32_t blk = 0; blk < (1u << 24); blk++) {
         uint64_t lo = (uint64_t)blk << 8, hi = lo + 255;
-        while (k + 1 < niv && t->iv_start[k + 1] <= lo) k++;
-        uint64_t next = (k + 1 < niv) ? t->iv_start[k + 1] : (1ull << 32);
+        while (k + 1 < niv && start[k + 1] <= lo) k++;
+        uint64_t next = (k + 1 < niv) ? start[k + 1] : (1ull << 32);
         if (next > hi) {
-            tbl24[blk] = dir_entry(t->iv_val[k]);
+            tbl24[blk] = entry[k];
             continue;
         }
         /* extended: paint the 256 addresses of this /24 from the intervals */
@@ -347,12 +374,87 @@ void cop_lpm_fill_dir24(const cop_lpm_table *t, uint32_t *tbl24, uint32_t *tbl8)
         uint32_t *grp = tbl8 + (size_t)g * 256;
         for (uint32_t a = 0; a < 256; a++) {
             uint64_t addr = lo + a;
-            while (kk + 1 < niv && t->iv_start[kk + 1] <= addr) kk++;
-            grp[a] = dir_entry(t->iv_val[kk]);
+            while (kk + 1 < niv && start[kk + 1] <= addr) kk++;
+            grp[a] = entry[kk];
         }
         tbl24[blk] = g | COP_DIR_VALID_EXT;
         g++;
     }
+}
+
+/* device entries of a form, one per (unmerged) interval */
+static uint32_t *form_entries(const cop_lpm_table *t, int form, const uint32_t **start, uint32_t *n)
+{
+    uint32_t cnt = form == COP_FORM_RULE ? t->n_rv : t->n_iv;
+    uint32_t *e = (uint32_t *)malloc((size_t)(cnt ? cnt : 1) * sizeof(uint32_t));
+    if (!e) return NULL;
+    for (uint32_t k = 0; k < cnt; k++)
+        e[k] = form == COP_FORM_RULE ? rule_entry(t, t->rv_rule[k]) : dir_entry(t->iv_val[k]);
+    *start = form == COP_FORM_RULE ? t->rv_start : t->iv_start;
+    *n = cnt;
+    return e;
+}
+
+void cop_lpm_fill_dir24(const cop_lpm_table *t, uint32_t *tbl24, uint32_t *tbl8)
+{
+    cop_lpm_form_fill_dir24(t, COP_FORM_NH, tbl24, tbl8);
+}
+
+void cop_lpm_form_fill_dir24(const cop_lpm_table *t, int form, uint32_t *tbl24, uint32_t *tbl8)
+{
+    const uint32_t *start;
+    uint32_t n;
+    uint32_t *e = form_entries(t, form, &start, &n);
+    if (!e) {   /* allocation failure: a table of misses (callers check n_ext) */
+        memset(tbl24, 0, sizeof(uint32_t) << 24);
+        return;
+    }
+    fill_dir24(start, e, n, tbl24, tbl8);
+    free(e);
+}
+
+uint32_t cop_lpm_form_n_ext(const cop_lpm_table *t, int form)
+{
+    return form == COP_FORM_RULE ? t->n_ext_rule : t->n_ext;
+}
+
+uint32_t cop_lpm_form_intervals(const cop_lpm_table *t, int form, uint32_t **starts, uint32_t **entries)
+{
+    if (form != COP_FORM_RULE) {
+        /* NH form: merged (nh | hit) values, as the interval export */
+        return cop_lpm_merged_intervals(t, starts, entries);
+    }
+    uint32_t *s = (uint32_t *)malloc((size_t)(t->n_rv ? t->n_rv : 1) * sizeof(uint32_t));
+    uint32_t *v = (uint32_t *)malloc((size_t)(t->n_rv ? t->n_rv : 1) * sizeof(uint32_t));
+    if (!s || !v) {
+        free(s);
+        free(v);
+        *starts = *entries = NULL;
+        return 0;
+    }
+    for (uint32_t k = 0; k < t->n_rv; k++) {
+        s[k] = t->rv_start[k];
+        v[k] = rule_entry(t, t->rv_rule[k]);
+    }
+    *starts = s;
+    *entries = v;
+    return t->n_rv;
+}
+
+int cop_lpm_lookup_rules(const cop_lpm_table *t, const uint32_t *ips, uint32_t n, int32_t *rule_id)
+{
+    if (!t || (n && (!ips || !rule_id))) return -EINVAL;
+    for (uint32_t i = 0; i < n; i++) {
+        /* last interval with start <= ip (rv_start[0] == 0) */
+        uint32_t lo = 0, hi = t->n_rv;
+        while (hi - lo > 1) {
+            uint32_t mid = lo + (hi - lo) / 2;
+            if (t->rv_start[mid] <= ips[i]) lo = mid;
+            else hi = mid;
+        }
+        rule_id[i] = t->rv_rule[lo] == COP_NO_RULE ? -1 : (int32_t)t->rv_rule[lo];
+    }
+    return 0;
 }
 
 int cop_lpm_export_dir24(const cop_lpm_table *t, uint32_t *tbl24, uint32_t *tbl8,

@@ -143,8 +143,13 @@ int  cop_lpm_export_dir24(const cop_lpm_table *t, uint32_t *tbl24, uint32_t *tbl
  * (hit << 24) | next_hop for addresses in [starts[k], starts[k+1]). */
 int  cop_lpm_export_intervals(const cop_lpm_table *t, uint32_t *starts, uint32_t *values,
                               uint32_t cap);
-/* Accepted rule set after all adds: masked prefix, depth, final next hop. */
+/* Accepted rule set after all adds: masked prefix, depth, final next hop.
+ * The position in this list is the rule id (first-acceptance order of the
+ * distinct (prefix, depth) pairs); per-rule hit counters are indexed by it. */
 int  cop_lpm_export_rules(const cop_lpm_table *t, cop_prefix *out, uint32_t cap);
+/* Host lookup of the matching (longest-prefix) rule id per address, -1 on a
+ * miss. Setup/diagnostic use; the data path runs on the GPU. */
+int  cop_lpm_lookup_rules(const cop_lpm_table *t, const uint32_t *ips, uint32_t n, int32_t *rule_id);
 
 /* ------------------------------------------------------------------------ */
 /* Rule files (rules.json format, firewall.c:57-105,276-323)                */
@@ -173,6 +178,7 @@ typedef struct cop_ctx cop_ctx;
 #define COP_CFG_FW_FORCE_DIR24  0x1u  /* FW lookups from the HBM DIR-24-8 image, not LDS */
 #define COP_CFG_LPM_FORCE_DIR24 0x2u  /* route lookups from HBM even if small */
 #define COP_CFG_NO_COMPACT      0x4u  /* never build the ordered forward list */
+#define COP_CFG_RULE_COUNTERS   0x8u  /* per-rule firewall hit counters (u64 per rule id) */
 
 typedef struct cop_config {
     int      device;          /* HIP device ordinal */
@@ -298,6 +304,33 @@ int  cop_counters_read(cop_ctx *ctx, cop_counters *out, int reset);
 /* Device address of the COP_COUNTER_SHARDS x COP_N_COUNTERS u64 counter
  * shards (an element-wise sum over GPUs preserves the per-shard layout). */
 void *cop_counters_device_ptr(cop_ctx *ctx);
+
+/* Per-rule firewall hit counters (COP_CFG_RULE_COUNTERS): one u64 per rule
+ * id of the firewall table (cop_lpm_export_rules order), incremented for
+ * every IPv4 packet whose source matches that rule in the FW stage (the
+ * rule rte_lpm_lookup resolved at firewall.c:194). Zeroed by
+ * cop_set_fw_table. read: copies min(cap, n_rules) words, returns n_rules
+ * (or -errno); reset != 0 zeroes them after the copy. */
+int  cop_rule_counters_read(cop_ctx *ctx, uint64_t *out, uint32_t cap, int reset);
+/* Device address and length of the per-rule counters. They sit directly
+ * after the COP_COUNTER_SHARDS x COP_N_COUNTERS shard words in one
+ * allocation, so one element-wise u64 sum covers both. */
+int  cop_rule_counters_device_ptr(cop_ctx *ctx, void **dptr, uint32_t *n_rules);
+
+/* Cross-GPU counter reduction over RCCL (xGMI): one communicator per
+ * context, one rank per GPU. The 128-byte unique id comes from rank 0's
+ * cop_coll_unique_id and is distributed by the caller (any transport).
+ * librccl is loaded on first use; -ENOSYS when it is absent. */
+#define COP_COLL_ID_BYTES 128
+int  cop_coll_unique_id(uint8_t id[COP_COLL_ID_BYTES]);
+int  cop_coll_init(cop_ctx *ctx, const uint8_t id[COP_COLL_ID_BYTES], int rank, int nranks);
+/* All-reduce (u64 sum) of the counter shards and per-rule counters of every
+ * rank, on the context's stream; synchronous. The sums are written to
+ * *total and rule_hits[0..min(cap, n_rules)) when non-NULL (cap = 0 skips
+ * the per-rule copy). reset != 0 zeroes this rank's local counters after
+ * the reduction (the read-and-zero of print_stats, switch.c:33-90). */
+int  cop_coll_reduce_counters(cop_ctx *ctx, cop_counters *total, uint64_t *rule_hits, uint32_t cap,
+                              int reset);
 
 /* Device memory helpers so C callers need no HIP headers. */
 int  cop_dev_alloc(cop_ctx *ctx, size_t bytes, void **dptr);

@@ -88,13 +88,22 @@ uint32_t orc_get_next_hop(const uint8_t *pkt, const uint16_t *rt)
 typedef struct orc_lpm {
     uint32_t max_rules, number_tbl8s;
     uint32_t n_rules;
-    /* rule table as a hash: key = depth<<32 | masked ip */
+    /* rule table as a hash: key = depth<<32 | masked ip; rid = rule id
+     * (order in which distinct rules were first accepted) */
     uint64_t *rkey;
     uint32_t *rnh;
+    uint32_t *rid;
     uint64_t rcap;
     uint32_t *tbl24;
     uint32_t *tbl8;
     uint8_t *grp_used;
+    /* rules-only mode (no DIR-24-8 image, for 1M-rule tables): tbl8 group
+     * accounting by the set of /24 parents holding a depth > 24 rule, and
+     * lookups by hash probes from depth 32 down */
+    int rules_only;
+    uint64_t *parents;
+    uint64_t pcap;
+    uint32_t n_groups;
 } orc_lpm;
 
 #define RK_EMPTY (~0ull)
@@ -136,37 +145,11 @@ static void rk_erase(orc_lpm *l, uint64_t slot)
         if (move) {
             l->rkey[i] = l->rkey[j];
             l->rnh[i] = l->rnh[j];
+            l->rid[i] = l->rid[j];
             l->rkey[j] = RK_EMPTY;
             i = j;
         }
     }
-}
-
-orc_lpm *orc_lpm_create(uint32_t max_rules, uint32_t number_tbl8s)
-{
-    if (max_rules == 0) return NULL;
-    orc_lpm *l = (orc_lpm *)calloc(1, sizeof(*l));
-    if (!l) return NULL;
-    l->max_rules = max_rules;
-    l->number_tbl8s = number_tbl8s;
-    l->rcap = 16;
-    while (l->rcap < 2ull * max_rules + 2) l->rcap <<= 1;
-    l->rkey = (uint64_t *)malloc(l->rcap * sizeof(uint64_t));
-    l->rnh = (uint32_t *)malloc(l->rcap * sizeof(uint32_t));
-    l->tbl24 = (uint32_t *)calloc((size_t)1 << 24, sizeof(uint32_t));
-    l->tbl8 = (uint32_t *)calloc((size_t)(number_tbl8s ? number_tbl8s : 1) * 256, sizeof(uint32_t));
-    l->grp_used = (uint8_t *)calloc(number_tbl8s ? number_tbl8s : 1, 1);
-    if (!l->rkey || !l->rnh || !l->tbl24 || !l->tbl8 || !l->grp_used) {
-        free(l->rkey);
-        free(l->rnh);
-        free(l->tbl24);
-        free(l->tbl8);
-        free(l->grp_used);
-        free(l);
-        return NULL;
-    }
-    memset(l->rkey, 0xFF, l->rcap * sizeof(uint64_t));
-    return l;
 }
 
 void orc_lpm_free(orc_lpm *l)
@@ -174,10 +157,65 @@ void orc_lpm_free(orc_lpm *l)
     if (!l) return;
     free(l->rkey);
     free(l->rnh);
+    free(l->rid);
     free(l->tbl24);
     free(l->tbl8);
     free(l->grp_used);
+    free(l->parents);
     free(l);
+}
+
+/* flags bit 0: rules-only mode (see struct orc_lpm) */
+orc_lpm *orc_lpm_create2(uint32_t max_rules, uint32_t number_tbl8s, uint32_t flags)
+{
+    if (max_rules == 0) return NULL;
+    orc_lpm *l = (orc_lpm *)calloc(1, sizeof(*l));
+    if (!l) return NULL;
+    l->max_rules = max_rules;
+    l->number_tbl8s = number_tbl8s;
+    l->rules_only = (flags & 1u) != 0;
+    l->rcap = 16;
+    while (l->rcap < 2ull * max_rules + 2) l->rcap <<= 1;
+    l->rkey = (uint64_t *)malloc(l->rcap * sizeof(uint64_t));
+    l->rnh = (uint32_t *)malloc(l->rcap * sizeof(uint32_t));
+    l->rid = (uint32_t *)malloc(l->rcap * sizeof(uint32_t));
+    int ok = l->rkey && l->rnh && l->rid;
+    if (l->rules_only) {
+        uint64_t want = number_tbl8s < max_rules ? number_tbl8s : max_rules;
+        l->pcap = 16;
+        while (l->pcap < 2 * want + 2) l->pcap <<= 1;
+        l->parents = (uint64_t *)malloc(l->pcap * sizeof(uint64_t));
+        ok = ok && l->parents;
+        if (l->parents) memset(l->parents, 0xFF, l->pcap * sizeof(uint64_t));
+    } else {
+        l->tbl24 = (uint32_t *)calloc((size_t)1 << 24, sizeof(uint32_t));
+        l->tbl8 = (uint32_t *)calloc((size_t)(number_tbl8s ? number_tbl8s : 1) * 256, sizeof(uint32_t));
+        l->grp_used = (uint8_t *)calloc(number_tbl8s ? number_tbl8s : 1, 1);
+        ok = ok && l->tbl24 && l->tbl8 && l->grp_used;
+    }
+    if (!ok) {
+        orc_lpm_free(l);
+        return NULL;
+    }
+    memset(l->rkey, 0xFF, l->rcap * sizeof(uint64_t));
+    return l;
+}
+
+orc_lpm *orc_lpm_create(uint32_t max_rules, uint32_t number_tbl8s)
+{
+    return orc_lpm_create2(max_rules, number_tbl8s, 0);
+}
+
+/* rules-only: does /24 parent p hold a group; insert when asked */
+static int parent_has(orc_lpm *l, uint64_t p, int insert)
+{
+    uint64_t i = rk_hash(p) & (l->pcap - 1);
+    while (l->parents[i] != RK_EMPTY) {
+        if (l->parents[i] == p) return 1;
+        i = (i + 1) & (l->pcap - 1);
+    }
+    if (insert) l->parents[i] = p;
+    return 0;
 }
 
 static int32_t tbl8_alloc(orc_lpm *l)
@@ -247,7 +285,24 @@ int orc_lpm_add(orc_lpm *l, uint32_t ip, uint32_t depth, uint32_t next_hop)
         if (l->n_rules == l->max_rules) return -ENOSPC;
         l->rkey[slot] = key;
         l->rnh[slot] = nh;
+        l->rid[slot] = l->n_rules;
         l->n_rules++;
+    }
+    if (l->rules_only) {
+        /* tbl8 accounting only: a depth > 24 rule in a /24 without a group
+         * takes the next group (groups are never freed: no deletes) */
+        if (depth > 24 && !parent_has(l, ipm >> 8, 0)) {
+            if (l->n_groups >= l->number_tbl8s) {
+                if (!existed) {
+                    rk_erase(l, slot);
+                    l->n_rules--;
+                }
+                return -ENOSPC;
+            }
+            parent_has(l, ipm >> 8, 1);
+            l->n_groups++;
+        }
+        return 0;
     }
     if (depth <= 24) {
         add_depth_small(l, ipm, depth, nh);
@@ -264,8 +319,30 @@ int orc_lpm_add(orc_lpm *l, uint32_t ip, uint32_t depth, uint32_t next_hop)
     return 0;
 }
 
+/* Longest match by hash probes from depth 32 down: the rule id, or -1.
+ * Independent of the DIR-24-8 image (works in both modes). */
+int32_t orc_lpm_match_rule(const orc_lpm *l, uint32_t ip, uint32_t *next_hop)
+{
+    for (int d = 32; d >= 1; d--) {
+        uint64_t slot;
+        uint32_t ipm = ip & (uint32_t)(0xFFFFFFFFull << (32 - d));
+        if (rk_find(l, ((uint64_t)d << 32) | ipm, &slot)) {
+            if (next_hop) *next_hop = l->rnh[slot];
+            return (int32_t)l->rid[slot];
+        }
+    }
+    if (next_hop) *next_hop = 0;
+    return -1;
+}
+
+void orc_lpm_match_rules(const orc_lpm *l, const uint32_t *ips, uint64_t n, int32_t *rule)
+{
+    for (uint64_t i = 0; i < n; i++) rule[i] = orc_lpm_match_rule(l, ips[i], NULL);
+}
+
 int orc_lpm_lookup(const orc_lpm *l, uint32_t ip, uint32_t *next_hop)
 {
+    if (l->rules_only) return orc_lpm_match_rule(l, ip, next_hop) >= 0 ? 0 : -ENOENT;
     uint32_t e = l->tbl24[ip >> 8];
     if ((e & (E_VALID | E_GROUP)) == (E_VALID | E_GROUP)) e = l->tbl8[(size_t)E_NH(e) * 256 + (ip & 0xFF)];
     *next_hop = E_NH(e);
@@ -286,6 +363,7 @@ uint32_t orc_lpm_n_rules(const orc_lpm *l) { return l->n_rules; }
 
 uint32_t orc_lpm_tbl8_used(const orc_lpm *l)
 {
+    if (l->rules_only) return l->n_groups;
     uint32_t u = 0;
     for (uint32_t g = 0; g < l->number_tbl8s; g++) u += l->grp_used[g];
     return u;
@@ -293,16 +371,16 @@ uint32_t orc_lpm_tbl8_used(const orc_lpm *l)
 
 int orc_lpm_rules(const orc_lpm *l, uint32_t *ip, uint8_t *depth, uint32_t *nh, uint32_t cap)
 {
-    uint32_t k = 0;
+    /* in rule id order */
+    if (cap < l->n_rules) return -ENOSPC;
     for (uint64_t i = 0; i < l->rcap; i++) {
         if (l->rkey[i] == RK_EMPTY) continue;
-        if (k >= cap) return -ENOSPC;
+        uint32_t k = l->rid[i];
         ip[k] = (uint32_t)l->rkey[i];
         depth[k] = (uint8_t)(l->rkey[i] >> 32);
         nh[k] = l->rnh[i];
-        k++;
     }
-    return (int)k;
+    return (int)l->n_rules;
 }
 
 const uint32_t *orc_lpm_tbl24(const orc_lpm *l) { return l->tbl24; }
@@ -386,11 +464,13 @@ int orc_fw_packet_handler(const uint8_t *pkt, const orc_lpm *lpm, orc_fw_stats *
 #define ORC_STAGE_LPM 4u
 
 /* One batch through the contract; results are 8-byte records
- * {verdict, flags, port, route_nh}; fwd[] lists FORWARD indices in order.
+ * {verdict, flags, port, route_nh}; fwd[] lists FORWARD indices in order;
+ * rule_hits[rule id] (optional) counts FW-stage hits per matching rule.
  * pkt i at base + (offsets ? offsets[i] : i*stride). Returns fwd count. */
 uint32_t orc_process(const uint8_t *base, const uint32_t *offsets, uint64_t stride, uint32_t n,
                      const uint16_t *rt, uint32_t n_ports, uint32_t stages, const orc_lpm *fw,
-                     const orc_lpm *route, uint8_t *results, uint32_t *fwd, uint64_t *counters)
+                     const orc_lpm *route, uint8_t *results, uint32_t *fwd, uint64_t *counters,
+                     uint64_t *rule_hits)
 {
     orc_fw_stats st = {0, 0, 0, 0};
     uint32_t nf = 0;
@@ -416,7 +496,11 @@ uint32_t orc_process(const uint8_t *base, const uint32_t *offsets, uint64_t stri
                 verdict = a ? ORC_DROP_FW : ORC_FORWARD;
                 if (a) st.pkt_drop++;
                 else st.pkt_accept++;
-                if (hit) flags |= 2;
+                if (hit) {
+                    flags |= 2;
+                    /* per-rule hit counter: the rule rte_lpm_lookup resolved */
+                    if (rule_hits) rule_hits[orc_lpm_match_rule(fw, be32at(p + 26), NULL)]++;
+                }
             }
             (void)before_not;
         }

@@ -36,6 +36,8 @@ def lib():
             "orc_route_table_default": (None, [c_void_p, c_uint32]),
             "orc_get_next_hop": (c_uint32, [c_void_p, c_void_p]),
             "orc_lpm_create": (c_void_p, [c_uint32, c_uint32]),
+            "orc_lpm_create2": (c_void_p, [c_uint32, c_uint32, c_uint32]),
+            "orc_lpm_match_rules": (None, [c_void_p, c_void_p, c_uint64, c_void_p]),
             "orc_lpm_free": (None, [c_void_p]),
             "orc_lpm_add": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32]),
             "orc_lpm_lookup": (c_int, [c_void_p, c_uint32, POINTER(c_uint32)]),
@@ -47,7 +49,7 @@ def lib():
             "orc_brute_lookup": (None, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_uint64, c_void_p,
                                         c_void_p]),
             "orc_process": (c_uint32, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_uint32, c_uint32,
-                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
             "orc_coprocessor_bench": (c_double, [c_void_p, c_uint64, c_void_p, c_double, c_int, c_int,
                                                  POINTER(c_uint64), POINTER(c_double)]),
         }
@@ -64,10 +66,13 @@ def _p(a):
 
 
 class OracleLpm:
-    """Incremental DIR-24-8 restatement of DPDK 17.11 rte_lpm."""
+    """Incremental DIR-24-8 restatement of DPDK 17.11 rte_lpm.
 
-    def __init__(self, max_rules=1024, number_tbl8s=24):
-        self.h = lib().orc_lpm_create(max_rules, number_tbl8s)
+    rules_only=True keeps the rule hash and tbl8 accounting but no DIR-24-8
+    image (lookups by hash probes, depth 32 down): the 1M-rule form."""
+
+    def __init__(self, max_rules=1024, number_tbl8s=24, rules_only=False):
+        self.h = lib().orc_lpm_create2(max_rules, number_tbl8s, 1 if rules_only else 0)
         if not self.h:
             raise MemoryError("orc_lpm_create")
 
@@ -113,6 +118,22 @@ class OracleLpm:
         order = np.lexsort((d, ip))
         return ip[order], d[order], nh[order]
 
+    def rules_by_id(self):
+        """Accepted rules indexed by rule id (first-acceptance order)."""
+        n = self.n_rules
+        ip = np.zeros(n, dtype=np.uint32)
+        d = np.zeros(n, dtype=np.uint8)
+        nh = np.zeros(n, dtype=np.uint32)
+        lib().orc_lpm_rules(self.h, _p(ip), _p(d), _p(nh), n)
+        return ip, d, nh
+
+    def match_rules(self, ips: np.ndarray) -> np.ndarray:
+        """Matching rule id per address by hash probes (-1 on a miss)."""
+        ips = np.ascontiguousarray(ips, dtype=np.uint32)
+        out = np.zeros(len(ips), dtype=np.int32)
+        lib().orc_lpm_match_rules(self.h, _p(ips), len(ips), _p(out))
+        return out
+
 
 def brute_lookup(rip, rdepth, rnh, ips):
     rip = np.ascontiguousarray(rip, dtype=np.uint32)
@@ -135,10 +156,13 @@ RESULT_DT = np.dtype([("verdict", "u1"), ("flags", "u1"), ("port", "<u2"), ("rou
 
 
 def process(pkts: np.ndarray, n: int, *, stride=64, offsets=None, rt=None, n_ports=5, stages=3,
-            fw: OracleLpm | None = None, route: OracleLpm | None = None):
-    """Per-packet contract over one batch -> (results, forward list, counters)."""
+            fw: OracleLpm | None = None, route: OracleLpm | None = None, rule_hits: np.ndarray | None = None):
+    """Per-packet contract over one batch -> (results, forward list, counters).
+    rule_hits (u64[fw.n_rules], optional) accumulates FW hits per rule id."""
     if rt is None:
         rt = route_table_default(n_ports)
+    if rule_hits is not None:
+        assert fw is not None and rule_hits.dtype == np.uint64 and len(rule_hits) >= fw.n_rules
     fw = fw or OracleLpm(1, 1)
     route = route or OracleLpm(1, 1)
     res = np.zeros(n, dtype=RESULT_DT)
@@ -146,7 +170,7 @@ def process(pkts: np.ndarray, n: int, *, stride=64, offsets=None, rt=None, n_por
     cnt = np.zeros(16, dtype=np.uint64)
     offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint32)
     k = lib().orc_process(_p(pkts), _p(offs), stride, n, _p(rt), n_ports, stages, fw.h, route.h, _p(res),
-                          _p(fwd), _p(cnt))
+                          _p(fwd), _p(cnt), _p(rule_hits))
     names = ["pkt_drop", "pkt_accept", "pkt_not_ipv4", "pkt_total", "parse_err", "no_port", "forward",
              "route_hit", "rx"]
     return res, fwd[:k], {nm: int(cnt[i]) for i, nm in enumerate(names)}

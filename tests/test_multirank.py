@@ -20,13 +20,17 @@ g = copdist.Group(rank, world, "gloo")
 fw = cg.gen_rules(0x5EED1004, 1000, cg.GEN_FW, 20)
 lpm = orc.OracleLpm(1024, 24); lpm.setup(fw["ip"], fw["depth"], fw["next_hop"])
 pk = cg.gen_trace(copdist.shard_seed(0x5EED0004, rank), 20000, fw)
-res, fwd, cnt = orc.process(pk, 20000, stages=3, fw=lpm)
+hits = np.zeros(lpm.n_rules, np.uint64)
+res, fwd, cnt = orc.process(pk, 20000, stages=3, fw=lpm, rule_hits=hits)
 names = sorted(cnt)
 tot = g.sum_u64(np.array([cnt[k] for k in names], dtype=np.uint64))
+htot = g.sum_u64(hits)   # per-rule counters: same layout on every rank
+uid = g.broadcast_bytes(bytes(range(128)) if rank == 0 else None)   # RCCL id distribution
+assert uid == bytes(range(128)), uid
 g.barrier()
 mx = g.max(float(rank + 1))
 if rank == 0:
-    print(json.dumps({"names": names, "sum": [int(x) for x in tot], "max": mx}))
+    print(json.dumps({"names": names, "sum": [int(x) for x in tot], "max": mx, "hits": [int(x) for x in htot]}))
 g.close()
 """
 
@@ -64,9 +68,11 @@ def test_two_rank_gloo_shards_and_reductions():
     lpm = orc.OracleLpm(1024, 24)
     lpm.setup(fw["ip"], fw["depth"], fw["next_hop"])
     want = np.zeros(len(got["names"]), dtype=np.int64)
+    whits = np.zeros(lpm.n_rules, np.uint64)
     for r in range(2):
         pk = cg.gen_trace(copdist.shard_seed(0x5EED0004, r), 20000, fw)
-        _, _, cnt = orc.process(pk, 20000, stages=3, fw=lpm)
+        _, _, cnt = orc.process(pk, 20000, stages=3, fw=lpm, rule_hits=whits)
         want += np.array([cnt[k] for k in got["names"]])
     assert list(want) == got["sum"]
+    assert [int(x) for x in whits] == got["hits"] and whits.sum() > 0
     assert want[got["names"].index("rx")] == 40000
