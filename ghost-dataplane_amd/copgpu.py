@@ -156,9 +156,11 @@ def lib():
     """Load libcopgpu.so (raises ImportError when it has not been built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"{LIB_PATH} not built (run make -C ghost-dataplane_amd)")
-        L = ctypes.CDLL(LIB_PATH)
+        # $COP_LIB: an alternative in-tree build of the same ABI (A/B runs)
+        path = os.environ.get("COP_LIB") or LIB_PATH
+        if not os.path.exists(path):
+            raise ImportError(f"{path} not built (run make -C ghost-dataplane_amd)")
+        L = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)
             f.restype = res

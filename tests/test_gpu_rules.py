@@ -102,7 +102,7 @@ def test_config5_scale_1m_rules_1m_prefixes(gpu_ctx_factory):
 def test_rccl_single_rank_reduce(gpu_ctx_factory):
     """The RCCL reduction path with one rank: the all-reduce result equals the
     local counters; reset zeroes them. (Multi-rank runs need one GPU per
-    rank: bench.py --workload fw_lpm_1m_rc on the 8-GPU node.)"""
+    rank: bench.py --workload fw_lpm_1m on the 8-GPU node.)"""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_RULE_COUNTERS)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
