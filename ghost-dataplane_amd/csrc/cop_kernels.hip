@@ -91,10 +91,11 @@ __device__ __forceinline__ uint32_t eyt_search(const uint32_t *tree, uint32_t le
         }                                                                                  \
     } while (0)
 
-template <int FW, int LPM, bool IMIX, int PPT>
+// experiment builds may raise the occupancy target (KDEFS=-DCOPK_WAVES_PER_EU=8)
 #ifndef COPK_WAVES_PER_EU
 #define COPK_WAVES_PER_EU 1
 #endif
+template <int FW, int LPM, bool IMIX, int PPT>
 __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const CopKParams p)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];

@@ -1,0 +1,92 @@
+"""GPU: large tables against the oracle.
+
+Tables above 8192 intervals leave LDS for the DIR-24-8 image in HBM (the
+firewall's with rule-id payload, the route stage's with next hops). Records
+must stay bit-identical with thousands of tbl8 groups, a /16 holding 6000
+host routes, /1 prefixes and the two ends of the address space — with the
+default mode selection and with FORCE_DIR24 set explicitly.
+"""
+import numpy as np
+import pytest
+
+import copgpu as cg
+import oracle as orc
+from helpers import assert_parity, gpu_run
+
+pytestmark = pytest.mark.gpu
+
+S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
+MODES = {"auto": 0, "forced": cg.CFG_FW_FORCE_DIR24 | cg.CFG_LPM_FORCE_DIR24}
+
+
+def dense_routes():
+    """A route set with one /16 holding 6000 host routes (6000 tbl8
+    groups' worth of structure in one /16), full-width prefixes and the two
+    ends of the address space."""
+    rng = np.random.default_rng(42)
+    base = cg.gen_rules(0x5EED2099, 30000, cg.GEN_ROUTES, 0)
+    hosts = np.zeros(6000, dtype=cg.PREFIX_DT)
+    hosts["ip"] = 0x0A140000 | rng.choice(65536, 6000, replace=False).astype(np.uint32)
+    hosts["depth"] = 32
+    hosts["next_hop"] = rng.integers(1, 1 << 24, 6000)
+    edge = np.zeros(6, dtype=cg.PREFIX_DT)
+    edge["ip"] = [0, 0x80000000, 0xFFFFFFFF, 0, 0x0A140000, 0xFFFF0000]
+    edge["depth"] = [1, 1, 32, 32, 16, 16]
+    edge["next_hop"] = [11, 12, 13, 14, 15, 16]
+    return np.concatenate([base, hosts, edge])
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_large_fw_and_routes(gpu_ctx_factory, mode):
+    fw_rules = cg.gen_rules(0x5EED1077, 20000, cg.GEN_FW, 0)
+    routes = dense_routes()
+    fwt = cg.LpmTable(fw_rules, 20000, 1 << 16, False)
+    rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
+    assert len(fwt.intervals()[0]) > 8192       # leaves LDS
+    ctx = gpu_ctx_factory(stages=S | F | L, flags=MODES[mode] | cg.CFG_RULE_COUNTERS)
+    ctx.set_fw_table(fwt)
+    ctx.set_route_lpm(rtt)
+    ofw = orc.OracleLpm(20000, 1 << 16)
+    ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=False)
+    ort = orc.OracleLpm(1 << 20, 1 << 16)
+    ort.setup(routes["ip"], routes["depth"], routes["next_hop"], stop_at_error=False)
+    n = 262144
+    pk = cg.gen_trace(0x5EED0077, n, fw_rules, routes)
+    # steer 1/8 of the destinations into the dense /16 and onto the edges
+    pk2 = pk.reshape(n, 64)
+    rng = np.random.default_rng(3)
+    sel = rng.choice(n, n // 8, replace=False)
+    d = (0x0A140000 | rng.integers(0, 65536, len(sel))).astype(np.uint32)
+    d[:4] = [0, 0xFFFFFFFF, 0x0A140000, 0x0A14FFFF]
+    pk2[sel, 30:34] = d.astype(">u4").view(np.uint8).reshape(-1, 4)
+    hits = np.zeros(ofw.n_rules, np.uint64)
+    ro, fo, co = orc.process(pk, n, stages=S | F | L, fw=ofw, route=ort, rule_hits=hits)
+    ctx.counters(reset=True)
+    rg, fg, _ = gpu_run(ctx, pk, n, batches=4)
+    assert_parity(rg, fg, ro, fo)
+    cgc = ctx.counters()
+    for k in co:
+        assert cgc[k] == co[k], (k, cgc[k], co[k])
+    assert np.array_equal(ctx.rule_counters(), hits)
+    # the dense /16 was actually exercised
+    dense = ((ro["flags"] & 1) == 1)[sel]
+    assert dense.mean() > 0.05
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+def test_large_table_all_addresses_of_a_dense_chunk(gpu_ctx_factory, mode):
+    """Every address of the dense /16 (65536 lookups) against the oracle."""
+    routes = dense_routes()
+    rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
+    ctx = gpu_ctx_factory(stages=S | L, flags=MODES[mode])
+    ctx.set_route_lpm(rtt)
+    ort = orc.OracleLpm(1 << 20, 1 << 16)
+    ort.setup(routes["ip"], routes["depth"], routes["next_hop"], stop_at_error=False)
+    n = 65536
+    pk = cg.gen_trace(0x5EED0078, n, None, routes, opts=cg.trace_opts(pct_non_ipv4=0))
+    pk2 = pk.reshape(n, 64)
+    d = (0x0A140000 + np.arange(n)).astype(np.uint32)
+    pk2[:, 30:34] = d.astype(">u4").view(np.uint8).reshape(-1, 4)
+    ro, fo, _ = orc.process(pk, n, stages=S | L, route=ort)
+    rg, fg, _ = gpu_run(ctx, pk, n)
+    assert_parity(rg, fg, ro, fo)
