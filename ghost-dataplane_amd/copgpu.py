@@ -93,6 +93,8 @@ SIGNATURES = {
     "cop_rules_load_json": (c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
     "cop_rules_free": (None, [c_void_p]),
     "cop_rules_write_json": (c_int, [c_char_p, c_void_p, c_uint32]),
+    "cop_rules_load_bin": (c_int, [c_char_p, POINTER(c_void_p), POINTER(c_uint32)]),
+    "cop_rules_write_bin": (c_int, [c_char_p, c_void_p, c_uint32]),
     "cop_route_table_default": (None, [c_void_p, c_uint32]),
     "cop_config_default": (None, [POINTER(Config)]),
     "cop_create": (c_int, [POINTER(Config), POINTER(c_void_p)]),
@@ -252,6 +254,23 @@ def rules_load_json(path: str) -> np.ndarray:
 def rules_write_json(path: str, rules: np.ndarray):
     rules = np.ascontiguousarray(rules, dtype=PREFIX_DT)
     _check(lib().cop_rules_write_json(path.encode(), _ptr(rules), len(rules)), what=f"write {path}")
+
+
+def rules_load_bin(path: str) -> np.ndarray:
+    """Binary prefix dump (cop_rules_load_bin) -> PREFIX_DT array."""
+    p = c_void_p()
+    n = c_uint32()
+    _check(lib().cop_rules_load_bin(path.encode(), byref(p), byref(n)), what=f"load {path}")
+    try:
+        buf = (ctypes.c_uint8 * (n.value * PREFIX_DT.itemsize)).from_address(p.value) if n.value else b""
+        return np.frombuffer(bytes(buf), dtype=PREFIX_DT).copy()
+    finally:
+        lib().cop_rules_free(p)
+
+
+def rules_write_bin(path: str, rules: np.ndarray):
+    rules = np.ascontiguousarray(rules, dtype=PREFIX_DT)
+    _check(lib().cop_rules_write_bin(path.encode(), _ptr(rules), len(rules)), what=f"write {path}")
 
 
 class LpmTable:

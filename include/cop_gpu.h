@@ -164,6 +164,12 @@ int  cop_rules_load_json(const char *path, cop_prefix **out, uint32_t *n);
 void cop_rules_free(cop_prefix *rules);
 /* Write rules pretty-printed with short lines (<255 chars, firewall.c:72,95). */
 int  cop_rules_write_json(const char *path, const cop_prefix *rules, uint32_t n);
+/* Binary prefix dump for large sets: 16-byte header ("CPRB", u32 version 1,
+ * u64 count) + count 12-byte cop_prefix records, little-endian, file order.
+ * load: *out malloc'd (free with cop_rules_free); -ENOENT (open), -EINVAL
+ * (magic, version, or size != header + count * 12), -ENOMEM, -EIO. */
+int  cop_rules_load_bin(const char *path, cop_prefix **out, uint32_t *n);
+int  cop_rules_write_bin(const char *path, const cop_prefix *rules, uint32_t n);
 
 /* Default vport routing table (read_config, init.c:40-84): all 0, entries
  * 0..n_ports-1 = UNKNOWN_PORT, entry (192.167.10.(i+1) & 0xFFFF) = i. */

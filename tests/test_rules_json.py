@@ -1,6 +1,7 @@
 """rules.json loading: the product's C loader (cop_rules_load_json) against
 the oracle's Python restatement of setup_rules/fw_config_parse_file
 (firewall.c:57-105, 276-323) on the reference fixture and edge cases."""
+import errno
 import os
 
 import numpy as np
@@ -79,3 +80,55 @@ def test_write_roundtrip_short_lines(tmp_path):
     assert a == [(int(r["ip"]), int(r["depth"]), int(r["next_hop"])) for r in rules]
     back = cg.rules_load_json(str(f))
     assert np.array_equal(back["ip"], rules["ip"])
+
+
+# ---- binary prefix dumps (cop_rules_load_bin / cop_rules_write_bin) ----
+
+def test_bin_round_trip_1m(tmp_path):
+    rules = cg.gen_rules(0x5EED1005, 1000000, cg.GEN_FW, 0)
+    p = str(tmp_path / "fw1m.bin")
+    cg.rules_write_bin(p, rules)
+    assert os.path.getsize(p) == 16 + 12 * len(rules)
+    back = cg.rules_load_bin(p)
+    for f in ("ip", "depth", "next_hop"):
+        assert np.array_equal(back[f], rules[f])
+    # the same table as from the in-memory rules (file order kept)
+    a = cg.LpmTable(rules[:50000], 50000, 1 << 16, False)
+    b = cg.LpmTable(back[:50000], 50000, 1 << 16, False)
+    assert np.array_equal(a.rules(), b.rules())
+
+
+def test_bin_matches_json(tmp_path):
+    rules = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
+    pj, pb = str(tmp_path / "r.json"), str(tmp_path / "r.bin")
+    cg.rules_write_json(pj, rules)
+    cg.rules_write_bin(pb, rules)
+    j, b = cg.rules_load_json(pj), cg.rules_load_bin(pb)
+    for f in ("ip", "depth", "next_hop"):
+        assert np.array_equal(j[f], b[f])
+
+
+def test_bin_empty_and_errors(tmp_path):
+    p = str(tmp_path / "e.bin")
+    cg.rules_write_bin(p, np.zeros(0, dtype=cg.PREFIX_DT))
+    assert len(cg.rules_load_bin(p)) == 0
+    good = str(tmp_path / "g.bin")
+    cg.rules_write_bin(good, cg.gen_rules(1, 10, cg.GEN_FW, 0))
+    raw = open(good, "rb").read()
+    cases = {
+        "magic": b"XPRB" + raw[4:],
+        "version": raw[:4] + (2).to_bytes(4, "little") + raw[8:],
+        "truncated": raw[:-1],
+        "trailing": raw + b"\0",
+        "count": raw[:8] + (11).to_bytes(8, "little") + raw[16:],
+        "short_header": raw[:10],
+    }
+    for name, data in cases.items():
+        q = str(tmp_path / f"{name}.bin")
+        open(q, "wb").write(data)
+        with pytest.raises(cg.CopError) as ei:
+            cg.rules_load_bin(q)
+        assert ei.value.code == -errno.EINVAL, name
+    with pytest.raises(cg.CopError) as ei:
+        cg.rules_load_bin(str(tmp_path / "missing.bin"))
+    assert ei.value.code == -errno.ENOENT
