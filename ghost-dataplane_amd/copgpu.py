@@ -111,6 +111,7 @@ SIGNATURES = {
     "cop_poll": (c_int, [c_void_p]),
     "cop_process_host": (c_int, [c_void_p, POINTER(c_void_p), c_uint32, c_void_p, c_void_p, c_void_p]),
     "cop_process_host_stream": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
+    "cop_set_host_threads": (c_int, [c_void_p, c_uint32]),
     "cop_counters_read": (c_int, [c_void_p, c_void_p, c_int]),
     "cop_counters_device_ptr": (c_void_p, [c_void_p]),
     "cop_rule_counters_read": (c_int, [c_void_p, c_void_p, c_uint32, c_int]),
@@ -481,6 +482,9 @@ class Context:
         _check(lib().cop_process_host(self.handle, ptrs, n, _ptr(res), _ptr(fwd), byref(cnt)), self,
                "process_host")
         return res, fwd[: cnt.value]
+
+    def set_host_threads(self, n: int):
+        _check(lib().cop_set_host_threads(self.handle, n), self, "set_host_threads")
 
     def process_host_stream(self, ptrs: np.ndarray, batch: int) -> np.ndarray:
         """Streaming end-to-end path over host packet addresses (u64 array)."""

@@ -16,6 +16,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "cop_gpu.h"
@@ -61,6 +64,79 @@ struct Lane {
     uint32_t n = 0;
 };
 
+// Host gather pool for the end-to-end path: the caller and n-1 persistent
+// workers each copy one contiguous slice of the 64-byte header lines into
+// pinned staging (scattered mbuf reads are DRAM-latency bound per thread).
+struct GatherPool {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, done_cv;
+    uint64_t gen = 0;
+    int pending = 0;
+    bool stop = false;
+    const void *const *src = nullptr;
+    uint8_t *dst = nullptr;
+    uint32_t n = 0;
+    int parts = 1;
+
+    static void slice(const void *const *src, uint8_t *dst, uint32_t n, int parts, int i)
+    {
+        const uint32_t lo = (uint32_t)((uint64_t)n * i / parts), hi = (uint32_t)((uint64_t)n * (i + 1) / parts);
+        for (uint32_t q = lo; q < hi; q++) memcpy(dst + (size_t)q * 64, src[q], 64);
+    }
+    void worker(int i)
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return stop || gen != seen; });
+            if (stop) return;
+            seen = gen;
+            const void *const *s_ = src;
+            uint8_t *d_ = dst;
+            const uint32_t n_ = n;
+            const int p_ = parts;
+            lk.unlock();
+            slice(s_, d_, n_, p_, i);
+            lk.lock();
+            if (--pending == 0) done_cv.notify_one();
+        }
+    }
+    void start(int nthreads)
+    {
+        parts = nthreads;
+        for (int i = 1; i < nthreads; i++) th.emplace_back(&GatherPool::worker, this, i);
+    }
+    void gather(const void *const *s_, uint8_t *d_, uint32_t n_)
+    {
+        if (th.empty() || n_ < 4096) {
+            slice(s_, d_, n_, 1, 0);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(m);
+            src = s_;
+            dst = d_;
+            n = n_;
+            pending = (int)th.size();
+            gen++;
+        }
+        cv.notify_all();
+        slice(s_, d_, n_, parts, 0);
+        std::unique_lock<std::mutex> lk(m);
+        done_cv.wait(lk, [&] { return pending == 0; });
+    }
+    ~GatherPool()
+    {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto &t : th) t.join();
+    }
+};
+
 }  // namespace
 
 struct cop_ctx {
@@ -102,6 +178,7 @@ struct cop_ctx {
     uint32_t *d_fwd = nullptr;
     uint32_t *d_fwdn = nullptr;
     uint32_t stage_cap = 0;
+    GatherPool *gather = nullptr;   // cop_set_host_threads
 };
 
 static int set_err(cop_ctx *c, int code, const char *fmt, ...)
@@ -205,6 +282,7 @@ void cop_destroy(cop_ctx *c)
     if (c->d_fwd) (void)hipFree(c->d_fwd);
     if (c->d_fwdn) (void)hipFree(c->d_fwdn);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c->gather;
     delete c;
 }
 
@@ -719,6 +797,12 @@ int cop_poll(cop_ctx *c)
     return 0;
 }
 
+static void host_gather(cop_ctx *c, const void *const *src, uint8_t *dst, uint32_t n)
+{
+    if (c->gather) c->gather->gather(src, dst, n);
+    else GatherPool::slice(src, dst, n, 1, 0);
+}
+
 int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_result *results,
                      uint32_t *fwd_idx, uint32_t *fwd_count)
 {
@@ -747,7 +831,7 @@ int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_re
     }
     if (int rc0 = sync_lanes(c)) return rc0;   // the staging buffers may still be in use
     // gather the first 64 bytes of every packet (headers the pipeline reads)
-    for (uint32_t i = 0; i < n; i++) memcpy(c->h_stage + (size_t)i * 64, pkt_data[i], 64);
+    host_gather(c, pkt_data, c->h_stage, n);
     HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, (size_t)n * 64, hipMemcpyHostToDevice, c->stream));
     cop_batch b;
     memset(&b, 0, sizeof(b));
@@ -768,6 +852,19 @@ int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_re
     if (rc) return rc;
     if (fwd_idx && cnt) HIPCHK(c, hipMemcpy(fwd_idx, c->d_fwd, (size_t)cnt * 4, hipMemcpyDeviceToHost));
     if (fwd_count) *fwd_count = cnt;
+    return 0;
+}
+
+int cop_set_host_threads(cop_ctx *c, uint32_t n)
+{
+    if (!c || n == 0 || n > 256) return -EINVAL;
+    delete c->gather;
+    c->gather = nullptr;
+    if (n > 1) {
+        c->gather = new (std::nothrow) GatherPool();
+        if (!c->gather) return -ENOMEM;
+        c->gather->start((int)n);
+    }
     return 0;
 }
 
@@ -809,7 +906,7 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
         if (int rc = lane_finish(c, L, results)) return rc;
         const uint32_t k = (uint32_t)((n - first) < batch ? (n - first) : batch);
         // host gather of the 64-byte header lines (overlaps the other lanes)
-        for (uint32_t i = 0; i < k; i++) memcpy(L.h_stage + (size_t)i * 64, pkt_data[first + i], 64);
+        host_gather(c, pkt_data + first, L.h_stage, k);
         HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * 64, hipMemcpyHostToDevice, L.s));
         cop_batch b;
         memset(&b, 0, sizeof(b));

@@ -283,6 +283,9 @@ int  cop_process_host(cop_ctx *ctx, const void *const *pkt_data, uint32_t n,
  * other lanes. results[i] for every packet. Synchronous on return. */
 int  cop_process_host_stream(cop_ctx *ctx, const void *const *pkt_data, uint64_t n, uint32_t batch,
                              cop_result *results);
+/* Host threads for the header gather of the two calls above: the calling
+ * thread plus n-1 persistent workers (default 1 = the caller alone). */
+int  cop_set_host_threads(cop_ctx *ctx, uint32_t n);
 
 /* Counters (u64, device-resident, summed over every submitted packet).
  * On the device they are kept in COP_COUNTER_SHARDS shards of

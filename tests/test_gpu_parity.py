@@ -232,11 +232,13 @@ def test_repeated_submits_epochs(gpu_ctx_factory):
     assert_parity(rg, fg, ro, fo)
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 4])
-def test_process_host_stream_lanes(gpu_ctx_factory, lanes):
-    """Streaming end-to-end host path over mbuf-like scattered buffers."""
+@pytest.mark.parametrize("lanes,threads", [(1, 1), (2, 1), (4, 1), (2, 8), (4, 3)])
+def test_process_host_stream_lanes(gpu_ctx_factory, lanes, threads):
+    """Streaming end-to-end host path over mbuf-like scattered buffers, with
+    the header gather on 1..8 host threads."""
     rules = fw1k()
     ctx = setup_ctx(gpu_ctx_factory, rules, n_streams=lanes)
+    ctx.set_host_threads(threads)
     n = 50000
     pk = cg.gen_trace(0x5EED0700, n, rules)
     stride = 2176

@@ -4,8 +4,9 @@ end in host memory ... pinned hipMemcpyAsync in and out"): packets sit in an
 mbuf-like host pool (NB_MBUF = 131072 buffers at 2176 B stride, data at
 128 B headroom, init.h:38-44); cop_process_host_stream gathers each batch's
 64-byte header lines into pinned staging, copies H2D, runs the pipeline,
-copies the 8-byte records D2H, with the lanes overlapping. Results of the
-first pool pass are checked bit-exactly against the oracle.
+copies the 8-byte records D2H, with the lanes overlapping; the gather runs
+on 1..16 host threads (cop_set_host_threads). Results of the first pool
+pass are checked bit-exactly against the oracle.
 """
 import os
 import sys
@@ -35,18 +36,19 @@ def main():
     o.setup(fw["ip"], fw["depth"], fw["next_hop"])
     ro, _, _ = orc.process(pk, NB_MBUF, stages=3, fw=o)
 
-    print(f"{'lanes':>5s} {'batch':>7s} {'Mpkt/s':>9s} {'GB/s H2D':>9s}  parity")
-    for lanes in (1, 2, 4):
+    print(f"{'lanes':>5s} {'thr':>3s} {'batch':>7s} {'Mpkt/s':>9s} {'GB/s H2D':>9s}  parity")
+    for lanes, threads in ((1, 1), (2, 1), (4, 1), (2, 4), (4, 4), (4, 8), (4, 16)):
         ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=lanes)
         ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
+        ctx.set_host_threads(threads)
         for batch in (16384, 65536, 262144):
             res = ctx.process_host_stream(ptrs[:NB_MBUF], batch)    # warm + parity
             ok = np.array_equal(res.view(np.uint8), ro.view(np.uint8))
             t0 = time.perf_counter()
             res = ctx.process_host_stream(ptrs, batch)
             dt = time.perf_counter() - t0
-            print(f"{lanes:5d} {batch:7d} {n / dt / 1e6:9.1f} {n * 64 / dt / 1e9:9.2f}  {'ok' if ok else 'MISMATCH'}",
-                  flush=True)
+            print(f"{lanes:5d} {threads:3d} {batch:7d} {n / dt / 1e6:9.1f} {n * 64 / dt / 1e9:9.2f}  "
+                  f"{'ok' if ok else 'MISMATCH'}", flush=True)
         ctx.close()
     # synchronous single-batch path (cop_process_host) for reference
     ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW)
