@@ -23,6 +23,8 @@ FORWARD, DROP_FW, DROP_PARSE, DROP_NOT_IPV4, DROP_NO_PORT = 0, 1, 2, 3, 4
 FLAG_ROUTE_HIT, FLAG_FW_HIT = 0x1, 0x2
 LPM_STOP_AT_FIRST_ERROR = 0x1
 CFG_FW_FORCE_DIR24, CFG_LPM_FORCE_DIR24, CFG_NO_COMPACT, CFG_RULE_COUNTERS = 0x1, 0x2, 0x4, 0x8
+CFG_DEMUX_PORTS, CFG_PORT_STATS = 0x10, 0x20
+MAX_DEMUX_PORTS = 8
 GEN_FW, GEN_ROUTES = 0, 1
 UNKNOWN_PORT = 0xFFFF
 
@@ -82,6 +84,14 @@ class NfStats(Structure):
                 ("tx_dropped", c_uint64)]
 
 
+class PortStats(Structure):
+    _fields_ = [("rx_packets", c_uint64), ("rx_dropped", c_uint64), ("tx_packets", c_uint64),
+                ("tx_dropped", c_uint64), ("nf_dropped", c_uint64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
 # every function declared in include/cop_gpu.h: name -> (restype, argtypes)
 SIGNATURES = {
     "cop_lpm_build": (c_int, [c_void_p, c_uint32, POINTER(LpmConfig), POINTER(c_void_p), POINTER(LpmReport)]),
@@ -115,6 +125,8 @@ SIGNATURES = {
     "cop_counters_read": (c_int, [c_void_p, c_void_p, c_int]),
     "cop_counters_device_ptr": (c_void_p, [c_void_p]),
     "cop_rule_counters_read": (c_int, [c_void_p, c_void_p, c_uint32, c_int]),
+    "cop_port_stats_read": (c_int, [c_void_p, POINTER(PortStats), c_uint32, c_int]),
+    "cop_counters_snapshot": (c_int, [c_void_p, c_void_p, POINTER(PortStats), c_uint32, c_int]),
     "cop_rule_counters_device_ptr": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint32)]),
     "cop_coll_unique_id": (c_int, [c_void_p]),
     "cop_coll_init": (c_int, [c_void_p, c_void_p, c_int, c_int]),
@@ -449,6 +461,20 @@ class Context:
 
     def counters_device_ptr(self) -> int:
         return lib().cop_counters_device_ptr(self.handle)
+
+    def port_stats(self, reset=False) -> list:
+        """Per-port coprocessor_stats (CFG_PORT_STATS), synchronous."""
+        arr = (PortStats * MAX_DEMUX_PORTS)()
+        n = _check(lib().cop_port_stats_read(self.handle, arr, MAX_DEMUX_PORTS, 1 if reset else 0), self,
+                   "port_stats")
+        return [arr[i].as_dict() for i in range(n)]
+
+    def snapshot(self, reset=False, ports=0):
+        """Live counters (+ per-port stats) without waiting for submitted work."""
+        c = np.zeros(16, dtype=np.uint64)
+        arr = (PortStats * MAX_DEMUX_PORTS)()
+        _check(lib().cop_counters_snapshot(self.handle, _ptr(c), arr, ports, 1 if reset else 0), self, "snapshot")
+        return {k: int(c[i]) for i, k in enumerate(COUNTER_NAMES)}, [arr[i].as_dict() for i in range(ports)]
 
     def rule_counters(self, reset=False) -> np.ndarray:
         """Per-rule FW hit counters (CFG_RULE_COUNTERS), indexed by rule id."""

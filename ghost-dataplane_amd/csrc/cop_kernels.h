@@ -11,7 +11,10 @@
 #define COPK_MAX_LAUNCH_BATCHES 1024   /* ring launches; ticket lines per lane buffer */
 #define COPK_COUNTER_SHARDS 64   /* 16 u64 per shard (128 B) */
 static_assert(sizeof(void *) == 8, "64-bit only");
-#define COPK_LDS_MISC_WORDS 80
+#define COPK_LDS_MISC_WORDS 80       /* counts, tile, prefix, counter reduction */
+#define COPK_LDS_MISC_EXT_WORDS 408  /* + per-port counts/prefixes (demux, port stats) */
+#define COPK_MAX_DEMUX_PORTS 8
+#define COPK_PORT_WORDS 16           /* per shard: 8 ports x {rx, tx} */
 #define COPK_STAMP_WG 65536
 
 #define COPK_TBL_OFF 0
@@ -85,6 +88,9 @@ struct CopKParams {
     unsigned long long *look;
     unsigned long long *counters;
     unsigned long long *rule_hits;     // per-rule FW hit counters or nullptr
+    unsigned long long *port_ctr;      // per-port {rx, tx} shards (port_stats)
+    uint32_t demux;                    // > 0: one ordered forward list per port (count = ports)
+    uint32_t port_stats;               // > 0: per-port counters for ports < port_stats
     uint32_t *err;
     unsigned long long *stamps;   // diagnostic phase stamps (dbg bit 8)
 };
@@ -94,6 +100,9 @@ extern "C" {
 #endif
 hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int imix, int ppt,
                        uint32_t grid, uint32_t lds_bytes, hipStream_t stream);
+// dst[i] = src[i] (atomic load) or atomic exchange with 0 when reset
+hipError_t copk_snapshot(unsigned long long *src, uint32_t n_words, unsigned long long *dst, int reset,
+                         hipStream_t stream);
 #ifdef __cplusplus
 }
 #endif

@@ -80,6 +80,68 @@ __device__ __forceinline__ uint32_t eyt_search(const uint32_t *tree, uint32_t le
     return i - (1u << levels);
 }
 
+// Decoupled look-back over one chain of tile granules (tile t at
+// chain[t * stride]): publish this tile's aggregate, read up to 64
+// predecessors per round (lane l reads tile qhi-l), consume the ready prefix
+// up to and including the nearest inclusive prefix, then publish the
+// inclusive value. Granules are {epoch:32, flag:2 (1 aggregate, 2 inclusive),
+// value:30}; a stale epoch counts as not ready. Spins are bounded and report
+// through the host-mapped error word. Whole wave; returns the exclusive prefix.
+__device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_t stride, uint32_t j, uint32_t agg,
+                                              uint32_t epoch, uint32_t *err, int lane)
+{
+    const unsigned long long ep = (unsigned long long)epoch << 32;
+    if (j == 0) {
+        if (lane == 0) lb_store(&chain[0], ep | (2ull << 30) | agg);
+        return 0;
+    }
+    if (lane == 0) lb_store(&chain[(size_t)j * stride], ep | (1ull << 30) | agg);
+    uint32_t excl = 0;
+    int qhi = (int)j - 1;
+    uint32_t spins = 0;
+    for (;;) {
+        const int idx = qhi - lane;
+        const bool inb = idx >= 0;
+        const unsigned long long v = inb ? lb_load(&chain[(size_t)idx * stride]) : 0ull;
+        const uint32_t flag = (uint32_t)(v >> 30) & 3u;
+        const bool ok = inb && (uint32_t)(v >> 32) == epoch && flag != 0u;
+        const unsigned long long m_incl = __ballot(ok && flag == 2u);
+        const unsigned long long m_bad = __ballot(inb && !ok);
+        const int first_incl = m_incl ? __ffsll((long long)m_incl) - 1 : 64;
+        const int first_bad = m_bad ? __ffsll((long long)m_bad) - 1 : 64;
+        const int upto = min(first_incl + 1, first_bad);
+        uint32_t val = lane < upto ? ((uint32_t)v & 0x3FFFFFFFu) : 0u;
+#pragma unroll
+        for (int off = 32; off; off >>= 1) val += __shfl_xor(val, off);
+        excl += val;
+        if (first_incl < first_bad) break;
+        qhi -= upto;
+        if (upto == 0) {
+            if (++spins > (1u << 22)) {       // bounded: never hang the GPU
+                if (lane == 0) *err = 1u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (lane == 0) lb_store(&chain[(size_t)j * stride], ep | (2ull << 30) | (excl + agg));
+    return excl;
+}
+
+// Inclusive scan of n <= 64 per-lane counts (lanes >= n hold 0); returns the
+// exclusive value for this lane, *agg = the total.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t c, int n, int lane, uint32_t *agg)
+{
+    uint32_t inc = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(inc, off);
+        if (lane >= off) inc += u;
+    }
+    *agg = __shfl(inc, n - 1);
+    return inc - c;
+}
+
 // diagnostic-only phase stamps (p.dbg bit 8): wave 0 lane 0 writes
 // s_memrealtime (100 MHz) per phase into a buffer nothing else reads
 #define STAMP(ph)                                                                          \
@@ -136,7 +198,7 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
         B.offsets = p.rg.offsets ? p.rg.offsets + (size_t)slot * p.rg.offsets_slot_words : nullptr;
         B.results = (uint2 *)p.rg.results + (size_t)slot * p.rg.results_slot;
         B.fwd_idx = p.rg.fwd_idx ? p.rg.fwd_idx + (size_t)slot * p.rg.fwd_slot : nullptr;
-        B.fwd_count = p.rg.fwd_count ? p.rg.fwd_count + slot : nullptr;
+        B.fwd_count = p.rg.fwd_count ? p.rg.fwd_count + (size_t)slot * (p.demux ? p.demux : 1u) : nullptr;
         B.n = p.rg.n;
         B.stride = p.rg.stride;
         B.data_off = p.rg.data_off;
@@ -331,8 +393,8 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
     }
 
     STAMP(4);
-    if (p.compact) {
-        // ---- ordered compaction ----
+    if (p.compact && !p.demux) {
+        // ---- ordered compaction: one forward list per batch ----
         unsigned long long bal[PPT];
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
@@ -343,54 +405,10 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
         if (wave == 0) {
             // tile-local exclusive scan over the (step, wave) counts
             constexpr int NQ = PPT * WAVES;
-            const uint32_t c = lane < NQ ? s_cnt[lane] : 0u;
-            uint32_t inc = c;
-#pragma unroll
-            for (int off = 1; off < NQ; off <<= 1) {
-                const uint32_t u = __shfl_up(inc, off);
-                if (lane >= off) inc += u;
-            }
-            const uint32_t agg = __shfl(inc, NQ - 1);
-            if (lane < NQ) s_cnt[lane] = inc - c;
-            const unsigned long long ep = (unsigned long long)p.epoch << 32;
-            unsigned long long *look = p.look + look_off;
-            uint32_t excl = 0;
-            if (j == 0) {
-                if (lane == 0) lb_store(&look[j], ep | (2ull << 30) | agg);
-            } else {
-                if (lane == 0) lb_store(&look[j], ep | (1ull << 30) | agg);
-                // decoupled look-back, 64 predecessors per round: lane l reads
-                // tile qhi-l; consume the ready prefix up to and including the
-                // nearest inclusive prefix.
-                int qhi = (int)j - 1;
-                uint32_t spins = 0;
-                for (;;) {
-                    const int idx = qhi - lane;
-                    const bool inb = idx >= 0;
-                    const unsigned long long v = inb ? lb_load(&look[idx]) : 0ull;
-                    const uint32_t flag = (uint32_t)(v >> 30) & 3u;
-                    const bool ok = inb && (uint32_t)(v >> 32) == p.epoch && flag != 0u;
-                    const unsigned long long m_incl = __ballot(ok && flag == 2u);
-                    const unsigned long long m_bad = __ballot(inb && !ok);
-                    const int first_incl = m_incl ? __ffsll((long long)m_incl) - 1 : 64;
-                    const int first_bad = m_bad ? __ffsll((long long)m_bad) - 1 : 64;
-                    const int upto = min(first_incl + 1, first_bad);
-                    uint32_t val = lane < upto ? ((uint32_t)v & 0x3FFFFFFFu) : 0u;
-#pragma unroll
-                    for (int off = 32; off; off >>= 1) val += __shfl_xor(val, off);
-                    excl += val;
-                    if (first_incl < first_bad) break;
-                    qhi -= upto;
-                    if (upto == 0) {
-                        if (++spins > (1u << 22)) {       // bounded: never hang the GPU
-                            if (lane == 0) *p.err = 1u;   // host-mapped error word
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                }
-                if (lane == 0) lb_store(&look[j], ep | (2ull << 30) | (excl + agg));
-            }
+            uint32_t agg;
+            const uint32_t ex = wave_excl_scan(lane < NQ ? s_cnt[lane] : 0u, NQ, lane, &agg);
+            if (lane < NQ) s_cnt[lane] = ex;
+            const uint32_t excl = look_back(p.look + look_off, 1u, j, agg, p.epoch, p.err, lane);
             if (lane == 0) {
                 *s_pref = excl;
                 if (B.fwd_count && j == B.ntiles - 1) *B.fwd_count = excl + agg;
@@ -407,6 +425,53 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
                         (uint32_t)(bal[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u));
                     __builtin_nontemporal_store(base + k * BLOCK + tid,
                                                 &B.fwd_idx[pref + s_cnt[k * WAVES + wave] + r]);
+                }
+            }
+        }
+    } else if (p.compact) {
+        // ---- demux: one ordered forward list per vport (the tx_q order of
+        // each port's coprocessor, switch.c:306-327 + 464-470). Port q's
+        // list is at fwd_idx + q*n, its length at fwd_count[q]. One
+        // look-back chain per port, the chains spread over the waves. ----
+        constexpr int NQ = PPT * WAVES;
+        const uint32_t K = p.demux;
+        volatile uint32_t *s_dq = misc + COPK_LDS_MISC_WORDS;        // [K][NQ]
+        volatile uint32_t *s_dpref = s_dq + COPK_MAX_DEMUX_PORTS * NQ; // [K]
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            for (uint32_t q = 0; q < K; q++) {
+                const unsigned long long b = __ballot(fwd[k] && port[k] == q);
+                if (lane == 0) s_dq[q * NQ + k * WAVES + wave] = (uint32_t)__popcll(b);
+            }
+        }
+        __syncthreads();
+        for (uint32_t q = (uint32_t)wave; q < K; q += WAVES) {
+            uint32_t agg;
+            const uint32_t ex = wave_excl_scan(lane < NQ ? s_dq[q * NQ + lane] : 0u, NQ, lane, &agg);
+            if (lane < NQ) s_dq[q * NQ + lane] = ex;
+            const uint32_t excl = look_back(p.look + (size_t)look_off * K + q, K, j, agg, p.epoch, p.err, lane);
+            if (lane == 0) {
+                s_dpref[q] = excl;
+                if (B.fwd_count && j == B.ntiles - 1) B.fwd_count[q] = excl + agg;
+            }
+        }
+        __syncthreads();
+        STAMP(5);
+        if (B.fwd_idx) {
+#pragma unroll
+            for (int k = 0; k < PPT; k++) {
+                uint32_t r = 0;
+                for (uint32_t q = 0; q < K; q++) {
+                    const bool mine = fwd[k] && port[k] == q;
+                    const unsigned long long b = __ballot(mine);
+                    if (mine)
+                        r = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+                }
+                if (fwd[k]) {
+                    const uint32_t q = port[k];
+                    __builtin_nontemporal_store(
+                        base + k * BLOCK + tid,
+                        &B.fwd_idx[(size_t)q * B.n + s_dpref[q] + s_dq[q * NQ + k * WAVES + wave] + r]);
                 }
             }
         }
@@ -453,6 +518,32 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
         if (v && !(p.dbg & 1u))
             atomicAdd(&p.counters[(blockIdx.x % COPK_COUNTER_SHARDS) * 16 + tid], (unsigned long long)v);
     }
+    if (p.port_stats) {
+        // per-port coprocessor_stats (switch.h:33-38): rx = packets routed to
+        // the port's NF (enqueue_nf_rx), tx = packets it forwarded
+        volatile uint32_t *s_ps = misc + COPK_LDS_MISC_WORDS + COPK_MAX_DEMUX_PORTS * PPT * WAVES + 8;
+        const uint32_t K = p.port_stats;
+        for (uint32_t q = 0; q < K; q++) {
+            uint32_t rx = 0, tx = 0;
+#pragma unroll
+            for (int k = 0; k < PPT; k++) {
+                rx += (uint32_t)__popcll(__ballot(valid[k] && port[k] == q));
+                tx += (uint32_t)__popcll(__ballot(fwd[k] && port[k] == q));
+            }
+            if (lane == 0) {
+                s_ps[wave * 16 + 2 * q] = rx;
+                s_ps[wave * 16 + 2 * q + 1] = tx;
+            }
+        }
+        __syncthreads();
+        if (tid < 2 * K) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int w = 0; w < WAVES; w++) v += s_ps[w * 16 + tid];
+            if (v) atomicAdd(&p.port_ctr[(blockIdx.x % COPK_COUNTER_SHARDS) * COPK_PORT_WORDS + tid],
+                             (unsigned long long)v);
+        }
+    }
     STAMP(6);
 }
 
@@ -495,4 +586,21 @@ extern "C" hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode
     if (fw_mode == COPK_TBL_IVT) return launch_lpm<COPK_TBL_IVT>(*p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
     if (fw_mode == COPK_TBL_DIR) return launch_lpm<COPK_TBL_DIR>(*p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
     return launch_lpm<COPK_TBL_OFF>(*p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
+}
+
+namespace {
+__global__ void cop_snapshot(unsigned long long *src, uint32_t n, unsigned long long *dst, int reset)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dst[i] = reset ? __hip_atomic_exchange(&src[i], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : __hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+} // namespace
+
+extern "C" hipError_t copk_snapshot(unsigned long long *src, uint32_t n_words, unsigned long long *dst, int reset,
+                                    hipStream_t stream)
+{
+    hipLaunchKernelGGL(cop_snapshot, dim3((n_words + 255) / 256), dim3(256), 0, stream, src, n_words, dst, reset);
+    return hipGetLastError();
 }

@@ -29,6 +29,10 @@
 namespace {
 
 constexpr uint32_t IVT_MAX = 8192;          // LDS interval entries per table (64 KiB)
+// counter block: [shards 64 x 16][port shards 64 x 16][per-rule words]
+constexpr size_t SHARD_WORDS = (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS;
+constexpr size_t PORT_WORDS = (size_t)COPK_COUNTER_SHARDS * COPK_PORT_WORDS;
+constexpr size_t RULE_OFF = SHARD_WORDS + PORT_WORDS;
 constexpr uint32_t LOOK_TILE_MIN = COPK_BLOCK;
 constexpr int TIMING_SLOTS = 256;   // per lane
 constexpr int MAX_LANES = 4;
@@ -179,6 +183,9 @@ struct cop_ctx {
     uint32_t *d_fwdn = nullptr;
     uint32_t stage_cap = 0;
     GatherPool *gather = nullptr;   // cop_set_host_threads
+    hipStream_t tele_stream = nullptr;  // cop_counters_snapshot
+    uint64_t *tele_host = nullptr;
+    unsigned long long *tele_dev = nullptr;
 };
 
 static int set_err(cop_ctx *c, int code, const char *fmt, ...)
@@ -282,6 +289,9 @@ void cop_destroy(cop_ctx *c)
     if (c->d_fwd) (void)hipFree(c->d_fwd);
     if (c->d_fwdn) (void)hipFree(c->d_fwdn);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->tele_stream) (void)hipStreamDestroy(c->tele_stream);
+    if (c->tele_host) (void)hipHostFree(c->tele_host);
+    if (c->tele_dev) (void)hipFree(c->tele_dev);
     delete c->gather;
     delete c;
 }
@@ -348,6 +358,8 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
         cfg.n_streams > MAX_LANES)
         return -EINVAL;
     if (cfg.n_streams == 0) cfg.n_streams = 1;
+    if ((cfg.flags & (COP_CFG_DEMUX_PORTS | COP_CFG_PORT_STATS)) && cfg.n_ports > COP_MAX_DEMUX_PORTS)
+        return -EINVAL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return -ENODEV;
     if (cfg.device < 0 || cfg.device >= ndev) return -ENODEV;
@@ -408,8 +420,8 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
         }
     }
     c->stream = c->lane[0].s;
-    CREATE_CHK(hipMalloc(&c->counters, COPK_COUNTER_SHARDS * COP_N_COUNTERS * 8));
-    CREATE_CHK(hipMemset(c->counters, 0, COPK_COUNTER_SHARDS * COP_N_COUNTERS * 8));
+    CREATE_CHK(hipMalloc(&c->counters, RULE_OFF * 8));
+    CREATE_CHK(hipMemset(c->counters, 0, RULE_OFF * 8));
     CREATE_CHK(hipHostMalloc(&c->h_err, 64, hipHostMallocMapped));
     c->h_err[0] = 0;
     CREATE_CHK(hipHostGetDevicePointer((void **)&c->d_err, c->h_err, 0));
@@ -504,11 +516,10 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
 // per-rule words; the shard words are carried over, the rule words zeroed
 static int resize_counters(cop_ctx *c, uint32_t n_rules)
 {
-    const size_t shard_words = (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS;
     unsigned long long *nb = nullptr;
-    HIPCHK(c, hipMalloc(&nb, (shard_words + n_rules) * 8));
-    hipError_t e = hipMemcpy(nb, c->counters, shard_words * 8, hipMemcpyDeviceToDevice);
-    if (e == hipSuccess && n_rules) e = hipMemset(nb + shard_words, 0, (size_t)n_rules * 8);
+    HIPCHK(c, hipMalloc(&nb, (RULE_OFF + n_rules) * 8));
+    hipError_t e = hipMemcpy(nb, c->counters, RULE_OFF * 8, hipMemcpyDeviceToDevice);
+    if (e == hipSuccess && n_rules) e = hipMemset(nb + RULE_OFF, 0, (size_t)n_rules * 8);
     if (e != hipSuccess) {
         (void)hipFree(nb);
         return set_err(c, -EIO, "counter resize: %s", hipGetErrorString(e));
@@ -570,7 +581,7 @@ static void harvest_one(cop_ctx *c, Lane &L)
     L.ev_count--;
 }
 
-static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb);
+static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb, bool demux);
 static int pick_mode(const cop_ctx *c, const DevLpm &t, bool enabled, bool force_dir);
 
 int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
@@ -579,7 +590,7 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
     if (nb == 0) return 0;
     Lane &L = c->lane[c->next_lane];
     c->next_lane = (c->next_lane + 1) % c->n_lanes;
-    return submit_on(c, L, batches, nb);
+    return submit_on(c, L, batches, nb, true);
 }
 
 static int choose_ppt(const cop_ctx *c, uint64_t total)
@@ -602,15 +613,16 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, int ppt, uin
     int lpm_mode =
         pick_mode(c, c->lpm, (stages & COP_STAGE_LPM) != 0, (c->cfg.flags & COP_CFG_LPM_FORCE_DIR24) != 0);
     HIPCHK(c, hipSetDevice(c->device));
-    if (p.ntiles > L.look_cap) {
+    const uint32_t look_need = p.ntiles * (p.demux ? p.demux : 1u);   // one chain per port (demux)
+    if (look_need > L.look_cap) {
         // grow this lane's look-back words (stream order: free after its work)
         HIPCHK(c, hipStreamSynchronize(L.s));
         HIPCHK(c, hipFree(L.look));
         L.look = nullptr;
         L.look_cap = 0;
-        HIPCHK(c, hipMalloc(&L.look, (size_t)p.ntiles * 8));
-        HIPCHK(c, hipMemset(L.look, 0, (size_t)p.ntiles * 8));
-        L.look_cap = p.ntiles;
+        HIPCHK(c, hipMalloc(&L.look, (size_t)look_need * 8));
+        HIPCHK(c, hipMemset(L.look, 0, (size_t)look_need * 8));
+        L.look_cap = look_need;
         L.epoch = 0;
     }
     p.stages = stages;
@@ -641,7 +653,7 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, int ppt, uin
     p.lds_lpm_off = off;
     off += 2 * p.lpm_m;
     p.lds_misc_off = off;
-    off += COPK_LDS_MISC_WORDS;
+    off += (p.demux || (c->cfg.flags & COP_CFG_PORT_STATS)) ? COPK_LDS_MISC_EXT_WORDS : COPK_LDS_MISC_WORDS;
     const uint32_t lds_bytes = off * 4;
     if (lds_bytes > 160 * 1024) return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_bytes);
     // tickets: draw from buffer `parity`, zero the other buffer's dirty lines
@@ -651,9 +663,9 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, int ppt, uin
     p.zero_lines = L.dirty[q ^ 1];
     p.look = L.look;
     p.counters = c->counters;
-    p.rule_hits = (fw_mode != COPK_TBL_OFF && c->n_rule_ctr)
-                      ? c->counters + (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS
-                      : nullptr;
+    p.rule_hits = (fw_mode != COPK_TBL_OFF && c->n_rule_ctr) ? c->counters + RULE_OFF : nullptr;
+    p.port_ctr = c->counters + SHARD_WORDS;
+    p.port_stats = (c->cfg.flags & COP_CFG_PORT_STATS) ? c->cfg.n_ports : 0u;
     p.err = c->d_err;
     p.stamps = c->stamps;
     if ((c->dbg & 8u) && p.ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
@@ -676,7 +688,9 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, int ppt, uin
     return 0;
 }
 
-static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb)
+// demux: the caller's forward lists follow the COP_CFG_DEMUX_PORTS layout
+// (public submits); the library's own host paths use one list per batch
+static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb, bool demux)
 {
     if (nb > c->cfg.max_batches) return set_err(c, -EINVAL, "nb %u > max_batches", nb);
     CopKParams p;
@@ -724,6 +738,7 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb)
     for (uint32_t i = 1; i < nb; i++)
         if (p.b[i].ntiles != p.b[0].ntiles) p.uniform_ntiles = 0;
     p.compact = compact ? 1u : 0u;
+    p.demux = (demux && compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 0u;
     return launch_on(c, L, p, imix, ppt, nb);
 }
 
@@ -739,9 +754,10 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     if (((uintptr_t)r->pkts & 15) || (r->pkts_slot_bytes & 15) || (r->data_off & 15) ||
         (!imix && ((r->stride & 15) || r->stride < 36)))
         return set_err(c, -EINVAL, "ring: packet starts must be 16-byte aligned");
-    if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < r->n))
-        return set_err(c, -EINVAL, "ring: slot sizes smaller than n");
     bool compact = (r->fwd_idx || r->fwd_count) && !(c->cfg.flags & COP_CFG_NO_COMPACT);
+    const uint32_t lists = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 1u;
+    if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < (uint64_t)r->n * lists))
+        return set_err(c, -EINVAL, "ring: slot sizes smaller than n (x ports with demux)");
     const int ppt = choose_ppt(c, (uint64_t)r->n * count);
     const uint32_t tile = COPK_BLOCK * ppt;
     const uint32_t tpb = r->n ? (r->n + tile - 1) / tile : 1;
@@ -766,6 +782,7 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     p.ntiles = tpb * count;
     p.uniform_ntiles = tpb;
     p.compact = compact ? 1u : 0u;
+    p.demux = lists > 1 || (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? lists : 0u;
     Lane &L = c->lane[c->next_lane];
     c->next_lane = (c->next_lane + 1) % c->n_lanes;
     return launch_on(c, L, p, imix, ppt, count);
@@ -841,7 +858,7 @@ int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_re
     b.results = c->d_res;
     b.fwd_idx = fwd_idx ? c->d_fwd : nullptr;
     b.fwd_count = (fwd_idx || fwd_count) ? c->d_fwdn : nullptr;
-    int rc = submit_on(c, c->lane[0], &b, 1);
+    int rc = submit_on(c, c->lane[0], &b, 1, false);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(results, c->d_res, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
     uint32_t cnt = 0;
@@ -914,7 +931,7 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
         b.n = k;
         b.stride = 64;
         b.results = L.d_res;
-        if (int rc = submit_on(c, L, &b, 1)) return rc;
+        if (int rc = submit_on(c, L, &b, 1, false)) return rc;
         HIPCHK(c, hipMemcpyAsync(L.h_res, L.d_res, (size_t)k * 8, hipMemcpyDeviceToHost, L.s));
         HIPCHK(c, hipEventRecord(L.done, L.s));
         L.busy = true;
@@ -946,12 +963,74 @@ int cop_counters_read(cop_ctx *c, cop_counters *out, int reset)
 
 void *cop_counters_device_ptr(cop_ctx *c) { return c ? (void *)c->counters : nullptr; }
 
+// fold the port shards into per-port coprocessor_stats
+static void fold_ports(const uint64_t *sh, cop_port_stats *out, uint32_t n)
+{
+    for (uint32_t q = 0; q < n; q++) {
+        uint64_t rx = 0, tx = 0;
+        for (int s = 0; s < COPK_COUNTER_SHARDS; s++) {
+            rx += sh[(size_t)s * COPK_PORT_WORDS + 2 * q];
+            tx += sh[(size_t)s * COPK_PORT_WORDS + 2 * q + 1];
+        }
+        memset(&out[q], 0, sizeof(out[q]));
+        out[q].rx_packets = rx;
+        out[q].tx_packets = tx;
+        out[q].nf_dropped = rx - tx;
+    }
+}
+
+static void fold_shards(const uint64_t *sh, cop_counters *out)
+{
+    uint64_t sum[COP_N_COUNTERS] = {0};
+    for (int s = 0; s < COPK_COUNTER_SHARDS; s++)
+        for (int k = 0; k < COP_N_COUNTERS; k++) sum[k] += sh[(size_t)s * COP_N_COUNTERS + k];
+    memcpy(out, sum, sizeof(cop_counters));
+}
+
+int cop_port_stats_read(cop_ctx *c, cop_port_stats *out, uint32_t n, int reset)
+{
+    if (!c || (n && !out)) return -EINVAL;
+    if (!(c->cfg.flags & COP_CFG_PORT_STATS)) return set_err(c, -EINVAL, "port stats not enabled");
+    if (n > c->cfg.n_ports) n = c->cfg.n_ports;
+    if (int rc = sync_lanes(c)) return rc;
+    std::vector<uint64_t> sh(PORT_WORDS);
+    HIPCHK(c, hipMemcpy(sh.data(), c->counters + SHARD_WORDS, PORT_WORDS * 8, hipMemcpyDeviceToHost));
+    fold_ports(sh.data(), out, n);
+    if (reset) HIPCHK(c, hipMemset(c->counters + SHARD_WORDS, 0, PORT_WORDS * 8));
+    return (int)c->cfg.n_ports;
+}
+
+// Live read(-and-zero) while launches are in flight: a small kernel on a
+// separate stream exchanges every counter word with 0 (or loads it) and the
+// copy goes to pinned memory; an increment lands either before the exchange
+// (this snapshot) or after it (the next one), none is lost.
+int cop_counters_snapshot(cop_ctx *c, cop_counters *total, cop_port_stats *ports, uint32_t n_ports, int reset)
+{
+    if (!c || (n_ports && !ports)) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->tele_stream) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->tele_stream, hipStreamNonBlocking));
+        HIPCHK(c, hipHostMalloc(&c->tele_host, RULE_OFF * 8, hipHostMallocDefault));
+        HIPCHK(c, hipMalloc(&c->tele_dev, RULE_OFF * 8));
+    }
+    hipError_t e = copk_snapshot(c->counters, (uint32_t)RULE_OFF, c->tele_dev, reset ? 1 : 0, c->tele_stream);
+    if (e != hipSuccess) return set_err(c, -EIO, "snapshot: %s", hipGetErrorString(e));
+    HIPCHK(c, hipMemcpyAsync(c->tele_host, c->tele_dev, RULE_OFF * 8, hipMemcpyDeviceToHost, c->tele_stream));
+    HIPCHK(c, hipStreamSynchronize(c->tele_stream));
+    if (total) fold_shards(c->tele_host, total);
+    if (n_ports) {
+        if (n_ports > c->cfg.n_ports) n_ports = c->cfg.n_ports;
+        fold_ports(c->tele_host + SHARD_WORDS, ports, n_ports);
+    }
+    return 0;
+}
+
 int cop_rule_counters_read(cop_ctx *c, uint64_t *out, uint32_t cap, int reset)
 {
     if (!c || (cap && !out)) return -EINVAL;
     if (!(c->cfg.flags & COP_CFG_RULE_COUNTERS)) return set_err(c, -EINVAL, "rule counters not enabled");
     if (int rc = sync_lanes(c)) return rc;
-    unsigned long long *d = c->counters + (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS;
+    unsigned long long *d = c->counters + RULE_OFF;
     const uint32_t k = cap < c->n_rule_ctr ? cap : c->n_rule_ctr;
     if (k) HIPCHK(c, hipMemcpy(out, d, (size_t)k * 8, hipMemcpyDeviceToHost));
     if (reset && c->n_rule_ctr) HIPCHK(c, hipMemset(d, 0, (size_t)c->n_rule_ctr * 8));
@@ -962,7 +1041,7 @@ int cop_rule_counters_device_ptr(cop_ctx *c, void **dptr, uint32_t *n_rules)
 {
     if (!c || !dptr) return -EINVAL;
     if (!(c->cfg.flags & COP_CFG_RULE_COUNTERS)) return set_err(c, -EINVAL, "rule counters not enabled");
-    *dptr = c->counters + (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS;
+    *dptr = c->counters + RULE_OFF;
     if (n_rules) *n_rules = c->n_rule_ctr;
     return 0;
 }
@@ -1037,8 +1116,8 @@ int cop_coll_reduce_counters(cop_ctx *c, cop_counters *total, uint64_t *rule_hit
     if (!c || (cap && !rule_hits)) return -EINVAL;
     if (!c->comm) return set_err(c, -EINVAL, "cop_coll_init not called");
     if (int rc = sync_lanes(c)) return rc;
-    const size_t shard_words = (size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS;
-    const size_t words = shard_words + c->n_rule_ctr;
+    const size_t shard_words = SHARD_WORDS;
+    const size_t words = RULE_OFF + c->n_rule_ctr;
     if (c->ctr_sum_words < words) {
         if (c->ctr_sum) (void)hipFree(c->ctr_sum);
         c->ctr_sum = nullptr;
@@ -1060,7 +1139,7 @@ int cop_coll_reduce_counters(cop_ctx *c, cop_counters *total, uint64_t *rule_hit
         memcpy(total, sum, sizeof(cop_counters));
     }
     const uint32_t k = cap < c->n_rule_ctr ? cap : c->n_rule_ctr;
-    if (k) HIPCHK(c, hipMemcpy(rule_hits, c->ctr_sum + shard_words, (size_t)k * 8, hipMemcpyDeviceToHost));
+    if (k) HIPCHK(c, hipMemcpy(rule_hits, c->ctr_sum + RULE_OFF, (size_t)k * 8, hipMemcpyDeviceToHost));
     return (int)c->n_rule_ctr;
 }
 

@@ -185,6 +185,16 @@ typedef struct cop_ctx cop_ctx;
 #define COP_CFG_LPM_FORCE_DIR24 0x2u  /* route lookups from HBM even if small */
 #define COP_CFG_NO_COMPACT      0x4u  /* never build the ordered forward list */
 #define COP_CFG_RULE_COUNTERS   0x8u  /* per-rule firewall hit counters (u64 per rule id) */
+/* Demux: one ordered forward list per vport instead of one per batch — the
+ * tx_q order of each port's coprocessor (enqueue_nf_rx switch.c:306-327,
+ * then coprocessor() switch.c:464-470). Port q's list is at fwd_idx + q*n
+ * (n = the batch's packet count), its length at fwd_count[q]; so fwd_idx
+ * holds n_ports*n entries and fwd_count n_ports (ring: fwd_slot >=
+ * n_ports*n, counts at fwd_count + slot*n_ports). Needs n_ports <= 8. */
+#define COP_CFG_DEMUX_PORTS     0x10u
+/* Per-port coprocessor_stats (switch.h:33-38) kept on the device. */
+#define COP_CFG_PORT_STATS      0x20u
+#define COP_MAX_DEMUX_PORTS     8
 
 typedef struct cop_config {
     int      device;          /* HIP device ordinal */
@@ -314,6 +324,29 @@ int  cop_counters_read(cop_ctx *ctx, cop_counters *out, int reset);
  * shards (an element-wise sum over GPUs preserves the per-shard layout). */
 void *cop_counters_device_ptr(cop_ctx *ctx);
 
+/* Per-port statistics (COP_CFG_PORT_STATS), mirroring struct
+ * coprocessor_stats (switch.h:33-38) of the NF serving each vport:
+ * rx_packets = packets routed to the port (enqueue_nf_rx), tx_packets =
+ * packets its NF forwarded, nf_dropped = rx - tx (freed by the NF). The
+ * ring-overflow drops (rx_dropped / tx_dropped) cannot occur on the device
+ * path and read 0. With stage P off every packet counts as port 0. */
+typedef struct cop_port_stats {
+    uint64_t rx_packets;
+    uint64_t rx_dropped;
+    uint64_t tx_packets;
+    uint64_t tx_dropped;
+    uint64_t nf_dropped;
+} cop_port_stats;
+/* Synchronous read of min(n, n_ports) ports; returns n_ports or -errno. */
+int  cop_port_stats_read(cop_ctx *ctx, cop_port_stats *out, uint32_t n, int reset);
+/* Live telemetry, the read-and-zero of print_stats (switch.c:33-90), safe
+ * while launches are in flight: counters (and port stats) are read — or
+ * atomically exchanged with 0 when reset — by a small kernel on a separate
+ * stream; no increment is lost or counted twice across snapshots. Does not
+ * wait for submitted work. */
+int  cop_counters_snapshot(cop_ctx *ctx, cop_counters *total, cop_port_stats *ports, uint32_t n_ports,
+                           int reset);
+
 /* Per-rule firewall hit counters (COP_CFG_RULE_COUNTERS): one u64 per rule
  * id of the firewall table (cop_lpm_export_rules order), incremented for
  * every IPv4 packet whose source matches that rule in the FW stage (the
@@ -321,9 +354,10 @@ void *cop_counters_device_ptr(cop_ctx *ctx);
  * cop_set_fw_table. read: copies min(cap, n_rules) words, returns n_rules
  * (or -errno); reset != 0 zeroes them after the copy. */
 int  cop_rule_counters_read(cop_ctx *ctx, uint64_t *out, uint32_t cap, int reset);
-/* Device address and length of the per-rule counters. They sit directly
- * after the COP_COUNTER_SHARDS x COP_N_COUNTERS shard words in one
- * allocation, so one element-wise u64 sum covers both. */
+/* Device address and length of the per-rule counters. One allocation holds
+ * the COP_COUNTER_SHARDS x COP_N_COUNTERS shard words, then the port-stat
+ * shards (COP_COUNTER_SHARDS x 16), then the per-rule words, so one
+ * element-wise u64 sum covers all three. */
 int  cop_rule_counters_device_ptr(cop_ctx *ctx, void **dptr, uint32_t *n_rules);
 
 /* Cross-GPU counter reduction over RCCL (xGMI): one communicator per

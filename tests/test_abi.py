@@ -62,6 +62,34 @@ def test_struct_layouts():
     assert cg.RESULT_DT.itemsize == 8
 
 
+def test_struct_layouts_match_c(tmp_path):
+    """Every struct the binding mirrors has the C compiler's size and field
+    offsets (compiled from include/cop_gpu.h)."""
+    mirrors = {"cop_batch": cg.Batch, "cop_batch_ring": cg.BatchRing, "cop_config": cg.Config,
+               "cop_lpm_config": cg.LpmConfig, "cop_lpm_report": cg.LpmReport, "cop_trace_opts": cg.TraceOpts,
+               "cop_nf_stats": cg.NfStats, "cop_port_stats": cg.PortStats}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "cop_gpu.h"', "int main(void){"]
+    for cname, py in mirrors.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append('printf("cop_counters size %zu\\n", sizeof(cop_counters));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    r = subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for cname, py in mirrors.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+    assert got[("cop_counters", "size")] == 16 * 8
+
+
 def test_no_gpu_fails_cleanly():
     if cg.device_count() > 0:
         return   # covered by the gpu tests
