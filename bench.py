@@ -58,16 +58,19 @@ def log(*a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=6720)
-    ap.add_argument("--warmup", type=int, default=960)
+    ap.add_argument("--steps", type=int, default=7680)
+    ap.add_argument("--warmup", type=int, default=1536)
     ap.add_argument("--workload", default="fw1k", choices=sorted(WORKLOADS))
-    ap.add_argument("--per-launch", type=int, default=96, help="batches per kernel launch (ring submit)")
+    ap.add_argument("--per-launch", type=int, default=384,
+                    help="batches per kernel launch (ring submit); 384 amortises the ~8 us launch ramp/tail")
     ap.add_argument("--streams", type=int, default=1, help="launch lanes (concurrent streams)")
-    ap.add_argument("--pool-mib", type=int, default=400, help="distinct input bytes per GPU")
+    ap.add_argument("--pool-mib", type=int, default=0,
+                    help="distinct input bytes per GPU (0: max(400 MiB, one launch of batches))")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-rule-counters", action="store_true", help="ablation: config 5 without per-rule counters")
     ap.add_argument("--stages", type=int, default=0, help="ablation: override the workload's stage mask")
+    ap.add_argument("--no-compact", action="store_true", help="ablation: no ordered forward lists")
     args = ap.parse_args()
 
     rank, world, local = copdist.env()
@@ -92,7 +95,7 @@ def main():
     if args.stages:
         W = dict(W, stages=args.stages)
     ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32, n_streams=args.streams,
-                     flags=cg.CFG_RULE_COUNTERS if rc_on else 0)
+                     flags=(cg.CFG_RULE_COUNTERS if rc_on else 0) | (cg.CFG_NO_COMPACT if args.no_compact else 0))
     ctx.set_fw_table(fw_tab)
     if rc_on:
         # RCCL communicator over the GPUs of the job (xGMI); id from rank 0 over gloo
@@ -110,6 +113,9 @@ def main():
         per_batch = slab.nbytes + offs.nbytes
     else:
         per_batch = B * 64
+    if not pool_bytes:
+        # > 256 MiB Infinity Cache, and at least one full launch of distinct batches
+        pool_bytes = max(400 << 20, per_batch * Lb)
     P = max(2, pool_bytes // per_batch)
     d_pkts = ctx.alloc(P * per_batch)
     d_res = ctx.alloc(P * B * 8)

@@ -408,7 +408,9 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
             uint32_t agg;
             const uint32_t ex = wave_excl_scan(lane < NQ ? s_cnt[lane] : 0u, NQ, lane, &agg);
             if (lane < NQ) s_cnt[lane] = ex;
-            const uint32_t excl = look_back(p.look + look_off, 1u, j, agg, p.epoch, p.err, lane);
+            // dbg bit 32 (timing-only ablation): no look-back wait, wrong offsets
+            const uint32_t excl =
+                (p.dbg & 32u) ? j * 1024u : look_back(p.look + look_off, 1u, j, agg, p.epoch, p.err, lane);
             if (lane == 0) {
                 *s_pref = excl;
                 if (B.fwd_count && j == B.ntiles - 1) *B.fwd_count = excl + agg;
