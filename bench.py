@@ -270,6 +270,17 @@ def main():
                        f"{secs:.1f} s on 1 pinned core (cpu {core})"),
         }
         log(f"[rank 0] cpu baseline {rate:.1f} Mpkt/s on 1 core ({pk} pkts)")
+        # one coprocessor thread per host core this job may
+        # use (the box's CPU share: OMP_NUM_THREADS, affinity), unpinned
+        ncores = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "8")), 32))
+        if ncores > 1:
+            rate_m, pk_m, secs_m = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget / 2, ncores, -1)
+            out["cpu_baseline_multicore"] = {
+                "value": round(rate_m, 3), "unit": "Mpkt/s", "cores": ncores, "kind": "port",
+                "sample": (f"{pk_m} packets, {ncores} threads each running the restated coprocessor() loop "
+                           f"on its own rings and mbuf pool, {secs_m:.1f} s"),
+            }
+            log(f"[rank 0] cpu baseline {rate_m:.1f} Mpkt/s on {ncores} cores")
 
     if rank == 0:
         print(json.dumps(out), flush=True)
