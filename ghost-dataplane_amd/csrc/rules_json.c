@@ -2,7 +2,11 @@
  * rules_json.c — rules.json loader/writer (host setup path).
  *
  * Restates setup_rules / fw_config_parse_file / fw_pkt_parse_ip
- * (firewall.c:32-55, 57-105, 276-323) without the vendored cJSON:
+ * (firewall.c:32-55, 57-105, 276-323) without the vendored cJSON, with
+ * cJSON 1.7.12's grammar (BOM, whitespace = any byte <= 32, strtod numbers
+ * over [0-9+-.eE], raw control bytes in strings, invalid \u hex = 0,
+ * trailing bytes after the root ignored); tests/test_ref_cjson.py pins it
+ * to the reference's own cJSON build:
  *   - the root's children, in file order, are the rules
  *     (fw_config_get_item_count firewall.c:107-127 counts them);
  *   - keys are matched case-insensitively, first match wins
@@ -61,7 +65,8 @@ static void skip_ws(jparser *ps)
 
 static jnode *parse_value(jparser *ps);
 
-static int hex4(const char *s, unsigned *out)
+/* cJSON parse_hex4: an invalid digit makes the whole value 0 */
+static unsigned hex4(const char *s)
 {
     unsigned v = 0;
     for (int i = 0; i < 4; i++) {
@@ -70,54 +75,58 @@ static int hex4(const char *s, unsigned *out)
         if (c >= '0' && c <= '9') v |= (unsigned)(c - '0');
         else if (c >= 'a' && c <= 'f') v |= (unsigned)(c - 'a' + 10);
         else if (c >= 'A' && c <= 'F') v |= (unsigned)(c - 'A' + 10);
-        else return -1;
+        else return 0;
     }
-    *out = v;
-    return 0;
+    return v;
 }
 
+/* cJSON parse_string: find the closing quote first (a backslash skips the
+ * next byte), then decode the escapes inside [start, end); \u sequences
+ * must fit before the closing quote. Control bytes are kept as they are. */
 static char *parse_string(jparser *ps)
 {
     if (ps->p >= ps->end || *ps->p != '"') return NULL;
-    const char *s = ++ps->p;
-    size_t cap = 16, len = 0;
-    char *out = (char *)malloc(cap);
-    if (!out) return NULL;
-    while (ps->p < ps->end && *ps->p != '"') {
-        unsigned cp;
-        char c = *ps->p++;
-        if (len + 5 >= cap) {
-            cap *= 2;
-            char *nb = (char *)realloc(out, cap);
-            if (!nb) goto fail;
-            out = nb;
+    const char *q = ps->p + 1;
+    while (q < ps->end && *q != '"') {
+        if (*q == '\\') {
+            if (q + 1 >= ps->end) return NULL;
+            q++;
         }
-        if (c != '\\') {
-            out[len++] = c;
+        q++;
+    }
+    if (q >= ps->end) return NULL;
+    const char *in = ps->p + 1, *end = q;
+    char *out = (char *)malloc((size_t)(end - in) + 1);
+    size_t len = 0;
+    if (!out) return NULL;
+    while (in < end) {
+        if (*in != '\\') {
+            out[len++] = *in++;
             continue;
         }
-        if (ps->p >= ps->end) goto fail;
-        c = *ps->p++;
-        switch (c) {
-        case 'b': out[len++] = '\b'; break;
-        case 'f': out[len++] = '\f'; break;
-        case 'n': out[len++] = '\n'; break;
-        case 'r': out[len++] = '\r'; break;
-        case 't': out[len++] = '\t'; break;
-        case '"': case '\\': case '/': out[len++] = c; break;
+        unsigned cp;
+        switch (in[1]) {
+        case 'b': out[len++] = '\b'; in += 2; break;
+        case 'f': out[len++] = '\f'; in += 2; break;
+        case 'n': out[len++] = '\n'; in += 2; break;
+        case 'r': out[len++] = '\r'; in += 2; break;
+        case 't': out[len++] = '\t'; in += 2; break;
+        case '"': case '\\': case '/': out[len++] = in[1]; in += 2; break;
         case 'u':
-            if (ps->end - ps->p < 4 || hex4(ps->p, &cp)) goto fail;
-            ps->p += 4;
+            if (end - in < 6) goto fail;
+            cp = hex4(in + 2);
+            if (cp >= 0xDC00 && cp <= 0xDFFF) goto fail;
             if (cp >= 0xD800 && cp <= 0xDBFF) {
-                unsigned lo;
-                if (ps->end - ps->p < 6 || ps->p[0] != '\\' || ps->p[1] != 'u' ||
-                    hex4(ps->p + 2, &lo) || lo < 0xDC00 || lo > 0xDFFF)
-                    goto fail;
-                ps->p += 6;
+                const char *sec = in + 6;
+                if (end - sec < 6 || sec[0] != '\\' || sec[1] != 'u') goto fail;
+                unsigned lo = hex4(sec + 2);
+                if (lo < 0xDC00 || lo > 0xDFFF) goto fail;
                 cp = 0x10000 + (((cp & 0x3FF) << 10) | (lo & 0x3FF));
-            } else if (cp >= 0xDC00 && cp <= 0xDFFF) {
-                goto fail;
+                in += 12;
+            } else {
+                in += 6;
             }
+            /* UTF-8; \u escapes expand to at most as many bytes as they take */
             if (cp < 0x80) {
                 out[len++] = (char)cp;
             } else if (cp < 0x800) {
@@ -138,10 +147,8 @@ static char *parse_string(jparser *ps)
             goto fail;
         }
     }
-    if (ps->p >= ps->end) goto fail;
-    ps->p++; /* closing quote */
-    out[len] = 0;
-    (void)s;
+    out[len] = 0;   /* a decoded \u0000 ends the C string, as in cJSON */
+    ps->p = end + 1;
     return out;
 fail:
     free(out);
@@ -310,6 +317,8 @@ int cop_rules_load_json(const char *path, cop_prefix **out, uint32_t *n_out)
     buf[got] = 0;
     /* the reference builds its buffer with fgets/strlen, so a NUL byte ends it */
     jparser ps = {buf, buf + strlen(buf), 0};
+    /* cJSON skip_utf8_bom (cJSON_ParseWithOpts) */
+    if (ps.end - ps.p >= 4 && !memcmp(ps.p, "\xEF\xBB\xBF", 3)) ps.p += 3;
     jnode *root = parse_value(&ps);
     free(buf);
     if (!root) return -EINVAL;

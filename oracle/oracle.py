@@ -13,8 +13,8 @@ against an independent brute-force LPM.
 from __future__ import annotations
 
 import ctypes
-import json
 import os
+import re
 from ctypes import POINTER, byref, c_double, c_int, c_uint8, c_uint32, c_uint64, c_void_p
 
 import numpy as np
@@ -226,43 +226,207 @@ def parse_ip(s: str):
     return ((vals[0] & 0xFF) << 24) | ((vals[1] & 0xFF) << 16) | ((vals[2] & 0xFF) << 8) | (vals[3] & 0xFF)
 
 
-def _valueint(v):
-    if v is True:
-        return 1
-    if isinstance(v, bool) or v is None or not isinstance(v, (int, float)):
+# cJSON 1.7.12 parser restatement (engine/thirdparty/cJSON.c): the grammar
+# the reference's rules loader actually accepts. Values are tuples:
+# ("obj", [(key, value), ...]) / ("arr", [...]) / ("str", bytes) /
+# ("num", float) / ("true",) / ("false",) / ("null",).
+
+class _CjsonFail(Exception):
+    pass
+
+
+_NUM_CHARS = b"0123456789+-eE."
+_STRTOD = re.compile(rb"[+-]?(?:\d+\.?\d*|\.\d+)(?:[eE][+-]?\d+)?")
+
+
+class _CjsonParser:
+    def __init__(self, data: bytes):
+        self.b = data + b"\0"          # buffer.length = strlen + 1 (cJSON_ParseWithOpts)
+        self.n = len(self.b)
+        self.i = 0
+        self.depth = 0
+
+    def ws(self):                       # buffer_skip_whitespace: every byte <= 32
+        while self.i < self.n and self.b[self.i] <= 32:
+            self.i += 1
+        if self.i == self.n:
+            self.i -= 1
+
+    def at(self, k=0):
+        return self.b[self.i + k] if self.i + k < self.n else None
+
+    def value(self):                    # parse_value
+        b, i = self.b, self.i
+        for lit, v in ((b"null", ("null",)), (b"false", ("false",)), (b"true", ("true",))):
+            if i + len(lit) <= self.n and b.startswith(lit, i):
+                self.i += len(lit)
+                return v
+        c = self.at()
+        if c == 0x22:
+            return ("str", self.string())
+        if c is not None and (c == 0x2D or 0x30 <= c <= 0x39):
+            return self.number()
+        if c == 0x5B:
+            return self.container(0x5B, 0x5D)
+        if c == 0x7B:
+            return self.container(0x7B, 0x7D)
+        raise _CjsonFail
+
+    def number(self):                   # parse_number: strtod over <= 63 number chars
+        j = self.i
+        while j < self.n and j - self.i < 63 and self.b[j] in _NUM_CHARS:
+            j += 1
+        m = _STRTOD.match(self.b[self.i:j])
+        if not m:
+            raise _CjsonFail
+        self.i += m.end()
+        return ("num", float(m.group(0)))
+
+    def string(self):                   # parse_string (+ utf16_literal_to_utf8)
+        b = self.b
+        if b[self.i] != 0x22:
+            raise _CjsonFail
+        end = self.i + 1
+        while end < self.n and b[end] != 0x22:
+            if b[end] == 0x5C:
+                if end + 1 >= self.n:
+                    raise _CjsonFail
+                end += 1
+            end += 1
+        if end >= self.n or b[end] != 0x22:
+            raise _CjsonFail
+        out = bytearray()
+        p = self.i + 1
+        esc = {ord("b"): 8, ord("f"): 12, ord("n"): 10, ord("r"): 13, ord("t"): 9, 0x22: 0x22, 0x5C: 0x5C, 0x2F: 0x2F}
+        while p < end:
+            if b[p] != 0x5C:
+                out.append(b[p])
+                p += 1
+                continue
+            c = b[p + 1]
+            if c in esc:
+                out.append(esc[c])
+                p += 2
+            elif c == ord("u"):
+                if end - p < 6:
+                    raise _CjsonFail
+                first = _hex4(b[p + 2:p + 6])
+                if 0xDC00 <= first <= 0xDFFF:
+                    raise _CjsonFail
+                if 0xD800 <= first <= 0xDBFF:
+                    q = p + 6
+                    if end - q < 6 or b[q] != 0x5C or b[q + 1] != ord("u"):
+                        raise _CjsonFail
+                    second = _hex4(b[q + 2:q + 6])
+                    if not 0xDC00 <= second <= 0xDFFF:
+                        raise _CjsonFail
+                    cp = 0x10000 + (((first & 0x3FF) << 10) | (second & 0x3FF))
+                    p += 12
+                else:
+                    cp = first
+                    p += 6
+                out += chr(cp).encode("utf-8", errors="surrogatepass")
+            else:
+                raise _CjsonFail
+        self.i = end + 1
+        return bytes(out).split(b"\0", 1)[0]    # valuestring is a C string
+
+    def container(self, open_c, close_c):   # parse_array / parse_object
+        if self.depth >= 1000:              # CJSON_NESTING_LIMIT
+            raise _CjsonFail
+        self.depth += 1
+        is_obj = open_c == 0x7B
+        items = []
+        self.i += 1
+        self.ws()
+        if self.at() == close_c:
+            self.i += 1
+            self.depth -= 1
+            return ("obj" if is_obj else "arr", items)
+        self.i -= 1
+        while True:
+            self.i += 1
+            self.ws()
+            if is_obj:
+                if self.at() != 0x22:
+                    raise _CjsonFail
+                key = self.string()
+                self.ws()
+                if self.at() != 0x3A:
+                    raise _CjsonFail
+                self.i += 1
+                self.ws()
+                items.append((key, self.value()))
+            else:
+                items.append(self.value())
+            self.ws()
+            if self.at() != 0x2C:
+                break
+        if self.at() != close_c:
+            raise _CjsonFail
+        self.i += 1
+        self.depth -= 1
+        return ("obj" if is_obj else "arr", items)
+
+
+def _hex4(h: bytes) -> int:             # parse_hex4: 0 on any invalid digit
+    try:
+        return int(h.decode("ascii"), 16) if len(h) == 4 and all(c in b"0123456789abcdefABCDEF" for c in h) else 0
+    except ValueError:
         return 0
-    if v >= INT_MAX:
-        return INT_MAX
-    if v <= INT_MIN:
-        return INT_MIN
-    return int(v)
+
+
+def cjson_parse(data: bytes):
+    """cJSON_Parse: BOM, whitespace, one value; trailing bytes ignored. None on failure."""
+    p = _CjsonParser(data)
+    if p.n > 4 and p.b.startswith(b"\xEF\xBB\xBF"):
+        p.i = 3
+    p.ws()
+    try:
+        return p.value()
+    except (_CjsonFail, IndexError):
+        return None
+
+
+def _valueint(v):
+    """cJSON valueint: saturated (int) of a number, 1 for true, else 0."""
+    if v[0] == "num":
+        x = v[1]
+        if x >= INT_MAX:
+            return INT_MAX
+        if x <= INT_MIN:
+            return INT_MIN
+        return int(x)
+    return 1 if v[0] == "true" else 0
+
+
+def _get_object_item(item, key: bytes):
+    """cJSON_GetObjectItem: first child whose name matches case-insensitively
+    (ASCII tolower); array elements have no name and never match."""
+    if item[0] != "obj":
+        return None
+    for k, v in item[1]:
+        if k.lower() == key:
+            return v
+    return None
 
 
 def load_rules_json(path: str):
-    """-> list of (ip, depth, action) with the reference's field semantics."""
+    """setup_rules (firewall.c:276-323) over the cJSON restatement ->
+    list of (ip, depth, action); ValueError where the reference calls
+    rte_exit or leaves src_ip uninitialised (fw_pkt_parse_ip failure)."""
     with open(path, "rb") as f:
-        text = f.read().split(b"\0", 1)[0].decode("utf-8", errors="surrogateescape")
-    root = json.loads(text, object_pairs_hook=lambda pairs: ("__obj__", pairs))
-    children = root[1] if isinstance(root, tuple) else (root if isinstance(root, list) else [])
-    if isinstance(root, tuple):
-        children = [v for _, v in children]
+        data = f.read().split(b"\0", 1)[0]       # json_str is a C string
+    root = cjson_parse(data)
+    if root is None:
+        raise ValueError("could not be parsed")
+    children = [v for _, v in root[1]] if root[0] == "obj" else (root[1] if root[0] == "arr" else [])
     out = []
     for c in children:
-        if not (isinstance(c, tuple) and c[0] == "__obj__"):
-            raise ValueError("rule is not an object")
-        pairs = c[1]
-
-        def get(key):
-            for k, v in pairs:
-                if k.lower() == key:
-                    return v, True
-            return None, False
-        ip, h1 = get("ip")
-        depth, h2 = get("depth")
-        action, h3 = get("action")
-        if not (h1 and h2 and h3) or not isinstance(ip, str):
-            raise ValueError("missing key / non-string ip")
-        v = parse_ip(ip)
+        ip, depth, action = (_get_object_item(c, k) for k in (b"ip", b"depth", b"action"))
+        if ip is None or depth is None or action is None:
+            raise ValueError("IP/Depth/Action not found")
+        v = parse_ip(ip[1].decode("utf-8", errors="surrogateescape")) if ip[0] == "str" else None
         if v is None:
             raise ValueError(f"bad ip {ip!r}")
         out.append((v, _valueint(depth) & 0xFF, _valueint(action) & 0xFF))

@@ -23,6 +23,8 @@ def _ensure_built():
         subprocess.run(["make", "-C", PKG, "-j8"], check=True)
     if not os.path.exists(os.path.join(ORACLE, "liboracle.so")):
         subprocess.run(["make", "-C", ORACLE], check=True)
+    if os.path.isdir("/root/reference") and not os.path.exists(os.path.join(ORACLE, "_ref", "libcjson_ref.so")):
+        subprocess.run(["make", "-C", ORACLE, "ref"], check=True)
 
 
 _ensure_built()
