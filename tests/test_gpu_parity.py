@@ -337,3 +337,81 @@ def test_ring_large_launch_many_batches(gpu_ctx_factory):
     fwd = df.download(np.uint32, n * P)
     got = np.concatenate([fwd[s * n: s * n + cnt[s]] + s * n for s in range(P)])
     assert np.array_equal(got, fo)
+
+
+@pytest.mark.parametrize("stride,data_off,n", [(2176, 128, 50000), (48, 0, 70000), (64, 16, 65536),
+                                               (128, 64, 262144)])
+def test_strides_and_data_off(gpu_ctx_factory, stride, data_off, n):
+    """Device-resident mbuf-like layouts: packet i at pkts + i*stride +
+    data_off (rte_pktmbuf_mtod), through cop_submit."""
+    rules = fw1k()
+    routes = routes100k(n=20000)
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L)
+    pk = cg.gen_trace(0x5EED0900 + stride, n, rules, routes)
+    slots = np.zeros((n, stride), dtype=np.uint8)
+    slots[:, data_off:data_off + min(64, stride - data_off)] = pk.reshape(n, 64)[:, :min(64, stride - data_off)]
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(slots.reshape(-1)[data_off:], n, stride=stride, stages=S | F | L, fw=fwo, route=rto)
+    dp = ctx.alloc(slots.nbytes)
+    dp.upload(slots.reshape(-1))
+    dr = ctx.alloc(n * 8)
+    df = ctx.alloc(n * 4)
+    dc = ctx.alloc(16)
+    ctx.submit([cg.make_batch(dp, n, dr, stride=stride, data_off=data_off, fwd_idx=df, fwd_count=dc)])
+    ctx.sync()
+    res = dr.download(cg.RESULT_DT, n)
+    cnt = int(dc.download(np.uint32, 1)[0])
+    assert_parity(res, df.download(np.uint32, cnt), ro, fo)
+
+
+def test_imix_with_data_off(gpu_ctx_factory):
+    rules = fw1k()
+    routes = routes100k(n=20000)
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L)
+    n = 30000
+    slab, offs = cg.gen_imix(0x5EED0A00, n, rules, routes)
+    # shift every packet 16 bytes further into its buffer: offsets stay, data_off = 16
+    slab2 = np.zeros(slab.nbytes + 64, dtype=np.uint8)
+    for i in range(0, n):
+        o = int(offs[i])
+        slab2[o + 16:o + 16 + 64] = slab[o:o + 64]
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(slab, n, offsets=offs, stages=S | F | L, fw=fwo, route=rto)
+    dp = ctx.alloc(slab2.nbytes)
+    dp.upload(slab2)
+    do = ctx.alloc(offs.nbytes)
+    do.upload(offs)
+    dr = ctx.alloc(n * 8)
+    df = ctx.alloc(n * 4)
+    dc = ctx.alloc(16)
+    ctx.submit([cg.make_batch(dp, n, dr, offsets=do, data_off=16, fwd_idx=df, fwd_count=dc)])
+    ctx.sync()
+    cnt = int(dc.download(np.uint32, 1)[0])
+    assert_parity(dr.download(cg.RESULT_DT, n), df.download(np.uint32, cnt), ro, fo)
+
+
+def test_misaligned_batches_rejected(gpu_ctx_factory):
+    ctx = gpu_ctx_factory(stages=S | F)
+    d = ctx.alloc(1 << 20)
+    for kw in (dict(stride=40), dict(stride=32), dict(data_off=8), dict(pkts_offset=4)):
+        with pytest.raises(cg.CopError):
+            ctx.submit([cg.make_batch(d, 1000, d, **kw)])
+    r = ctx.alloc(1 << 16)
+    with pytest.raises(cg.CopError):     # results must be 8-byte aligned
+        ctx.submit([cg.make_batch(d, 10, r.addr + 4)])
+
+
+@pytest.mark.parametrize("ppt", ["1", "4", "8"])
+def test_every_tile_width_same_records(gpu_ctx_factory, monkeypatch, ppt):
+    """The three kernel instantiations (PPT 1/4/8 packets per lane) on the
+    same 3 batches give the same, oracle-exact records and lists."""
+    monkeypatch.setenv("COP_PPT", ppt)
+    rules = fw1k()
+    routes = routes100k(n=20000)
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L)
+    n = 150001
+    pk = cg.gen_trace(0x5EED0B00, n, rules, routes)
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(pk, n, stages=S | F | L, fw=fwo, route=rto)
+    rg, fg, _ = gpu_run(ctx, pk, n, batches=3)
+    assert_parity(rg, fg, ro, fo)
