@@ -1,0 +1,656 @@
+// cop_device.h — device-side pieces shared by the two pipeline kernels
+// (cop_kernels.hip: one tile per workgroup; cop_stream.hip: persistent
+// streaming). Internal.
+//
+// Per packet, the classification restates (SURVEY.md §8a contract):
+//   stage P   get_next_hop            switch.c:93-136  (+ fast-path drop
+//             switch.c:406-410, enqueue_nf_rx port bound switch.c:316-319)
+//   stage FW  fw_packet_handler       firewall.c:170-213, lookup =
+//             rte_lpm_lookup(lpm_tbl, ntohl(src))     firewall.c:194
+//   stage LPM route rte_lpm semantics on ntohl(dst)   (north-star extension)
+// and the ordered compaction keeps FORWARD packets in arrival order, the
+// order coprocessor() hands them to enqueue_nf_tx (switch.c:464-470).
+#ifndef COP_DEVICE_H
+#define COP_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cop_kernels.h"
+
+namespace copd {
+
+constexpr int BLOCK = COPK_BLOCK;
+constexpr int WAVES = BLOCK / 64;
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ void lb_store(unsigned long long *p, unsigned long long v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ unsigned long long lb_load(unsigned long long *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void lds_stage(uint32_t *lds_dst, const void *gsrc, uint32_t n16, int lane, int wave)
+{
+    // one 1 KiB piece per wave-instruction: LDS destination = base + lane*16
+    const uint4 *g = (const uint4 *)gsrc;
+    for (uint32_t c = (uint32_t)wave; c * 64u < n16; c += WAVES) {
+        const uint32_t i = c * 64u + (uint32_t)lane;
+        if (i < n16)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(g + i),
+                                             (__attribute__((address_space(3))) void *)(lds_dst + c * 256u),
+                                             16, 0, 0);
+    }
+}
+
+// Interval search in LDS over an Eytzinger (BFS-order) tree: tree[1..m-1]
+// holds the sorted interval starts s[1..m-1] (s[0] == 0 is implicit), m a
+// power of two, padding starts 0xFFFFFFFF. Returns k = #{j >= 1 : s[j] <= ip},
+// the index of the interval holding ip. The top levels of the tree sit in
+// consecutive LDS words, so the first steps of 64 searches are broadcasts or
+// conflict-free, unlike a sorted-array search whose step-s probes all share
+// one bank.
+__device__ __forceinline__ uint32_t eyt_search(const uint32_t *tree, uint32_t levels, uint32_t ip)
+{
+    uint32_t i = 1;
+    for (uint32_t l = 0; l < levels; l++) i = 2u * i + (tree[i] <= ip ? 1u : 0u);
+    return i - (1u << levels);
+}
+
+// Decoupled look-back over one chain of tile granules (tile t at
+// chain[t * stride]): publish this tile's aggregate, read up to 64
+// predecessors per round (lane l reads tile qhi-l), consume the ready prefix
+// up to and including the nearest inclusive prefix, then publish the
+// inclusive value. Granules are {epoch:32, flag:2 (1 aggregate, 2 inclusive),
+// value:30}; a stale epoch counts as not ready. Spins are bounded and report
+// through the host-mapped error word. Whole wave; returns the exclusive prefix.
+__device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_t stride, uint32_t j, uint32_t agg,
+                                              uint32_t epoch, uint32_t *err, int lane)
+{
+    const unsigned long long ep = (unsigned long long)epoch << 32;
+    if (j == 0) {
+        if (lane == 0) lb_store(&chain[0], ep | (2ull << 30) | agg);
+        return 0;
+    }
+    if (lane == 0) lb_store(&chain[(size_t)j * stride], ep | (1ull << 30) | agg);
+    uint32_t excl = 0;
+    int qhi = (int)j - 1;
+    uint32_t spins = 0;
+    for (;;) {
+        const int idx = qhi - lane;
+        const bool inb = idx >= 0;
+        const unsigned long long v = inb ? lb_load(&chain[(size_t)idx * stride]) : 0ull;
+        const uint32_t flag = (uint32_t)(v >> 30) & 3u;
+        const bool ok = inb && (uint32_t)(v >> 32) == epoch && flag != 0u;
+        const unsigned long long m_incl = __ballot(ok && flag == 2u);
+        const unsigned long long m_bad = __ballot(inb && !ok);
+        const int first_incl = m_incl ? __ffsll((long long)m_incl) - 1 : 64;
+        const int first_bad = m_bad ? __ffsll((long long)m_bad) - 1 : 64;
+        const int upto = min(first_incl + 1, first_bad);
+        uint32_t val = lane < upto ? ((uint32_t)v & 0x3FFFFFFFu) : 0u;
+#pragma unroll
+        for (int off = 32; off; off >>= 1) val += __shfl_xor(val, off);
+        excl += val;
+        if (first_incl < first_bad) break;
+        qhi -= upto;
+        if (upto == 0) {
+            if (++spins > (1u << 22)) {       // bounded: never hang the GPU
+                if (lane == 0) *err = 1u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (lane == 0) lb_store(&chain[(size_t)j * stride], ep | (2ull << 30) | (excl + agg));
+    return excl;
+}
+
+// Segmented decoupled look-back over K <= 8 chains at once (one per vport
+// with demux, else one): lanes [q*seg, (q+1)*seg) resolve chain q, seg =
+// 64 / next_pow2(K) predecessors per round. Granule g of chain q sits at
+// chain[g*K + q], format as look_back(). The caller has already published
+// granule gi's aggregates (lb_publish); this resolves them: returns, in
+// every lane of group q, the exclusive prefix of chain q, and publishes the
+// inclusive value agg + prefix. agg: chain q's aggregate in group q's lanes.
+__device__ __forceinline__ uint32_t look_back_seg(unsigned long long *chain, uint32_t K, uint32_t gi, uint32_t agg,
+                                                  uint32_t epoch, uint32_t *err, int lane)
+{
+    const uint32_t seg = K == 1 ? 64u : K == 2 ? 32u : K <= 4 ? 16u : 8u;
+    const uint32_t q = (uint32_t)lane / seg, r = (uint32_t)lane % seg;
+    const bool active = q < K;
+    const unsigned long long segm = seg == 64 ? ~0ull : ((1ull << seg) - 1ull) << (q * seg);
+    const uint32_t sh = seg == 64 ? 0u : q * seg;
+    const unsigned long long ep = (unsigned long long)epoch << 32;
+    uint32_t excl = 0;
+    int qhi = (int)gi - 1;
+    bool done = !active || gi == 0;
+    uint32_t spins = 0;
+    while (__ballot(!done)) {
+        const int idx = qhi - (int)r;
+        const bool inb = !done && idx >= 0;
+        const unsigned long long v = inb ? lb_load(&chain[(size_t)idx * K + q]) : 0ull;
+        const uint32_t flag = (uint32_t)(v >> 30) & 3u;
+        const bool ok = inb && (uint32_t)(v >> 32) == epoch && flag != 0u;
+        const unsigned long long mi = (__ballot(ok && flag == 2u) & segm) >> sh;
+        const unsigned long long mb = (__ballot(inb && !ok) & segm) >> sh;
+        const uint32_t first_incl = mi ? (uint32_t)__ffsll((long long)mi) - 1u : seg;
+        const uint32_t first_bad = mb ? (uint32_t)__ffsll((long long)mb) - 1u : seg;
+        const uint32_t upto = min(first_incl + 1u, first_bad);
+        uint32_t val = (inb && r < upto) ? ((uint32_t)v & 0x3FFFFFFFu) : 0u;
+        for (uint32_t off = seg >> 1; off; off >>= 1) val += __shfl_xor(val, (int)off);
+        bool stalled = false;
+        if (!done) {
+            excl += val;
+            if (first_incl < first_bad) {
+                done = true;
+            } else {
+                qhi -= (int)upto;
+                stalled = upto == 0;
+            }
+        }
+        if (__ballot(stalled)) {
+            if (++spins > (1u << 22)) {       // bounded: never hang the GPU
+                if (lane == 0) *err = 1u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (active && r == 0 && gi != 0) lb_store(&chain[(size_t)gi * K + q], ep | (2ull << 30) | (excl + agg));
+    return excl;
+}
+
+// Publish granule gi's aggregates (lane q < K: chain q's agg_q): inclusive
+// at once for the batch's first granule, else an aggregate.
+__device__ __forceinline__ void lb_publish(unsigned long long *chain, uint32_t K, uint32_t gi, uint32_t agg_q,
+                                           uint32_t epoch, int lane)
+{
+    if ((uint32_t)lane < K)
+        lb_store(&chain[(size_t)gi * K + (uint32_t)lane],
+                 ((unsigned long long)epoch << 32) | ((gi == 0 ? 2ull : 1ull) << 30) | agg_q);
+}
+
+// Inclusive scan of n <= 64 per-lane counts (lanes >= n hold 0); returns the
+// exclusive value for this lane, *agg = the total.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t c, int n, int lane, uint32_t *agg)
+{
+    uint32_t inc = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(inc, off);
+        if (lane >= off) inc += u;
+    }
+    *agg = __shfl(inc, n - 1);
+    return inc - c;
+}
+
+// The batch a workgroup works on: a ring slot (ring launches) or a
+// descriptor (kernarg). *look_off = the batch's first look-back granule.
+__device__ __forceinline__ CopKBatch batch_desc(const CopKParams &p, uint32_t b, uint32_t *look_off)
+{
+    CopKBatch B;
+    if (p.ring) {
+        const uint32_t slot = (p.rg.first + b) % p.rg.n_slots;   // count may exceed n_slots
+        B.pkts = p.rg.pkts + (size_t)slot * p.rg.pkts_slot_bytes;
+        B.offsets = p.rg.offsets ? p.rg.offsets + (size_t)slot * p.rg.offsets_slot_words : nullptr;
+        B.results = (uint2 *)p.rg.results + (size_t)slot * p.rg.results_slot;
+        B.fwd_idx = p.rg.fwd_idx ? p.rg.fwd_idx + (size_t)slot * p.rg.fwd_slot : nullptr;
+        B.fwd_count = p.rg.fwd_count ? p.rg.fwd_count + (size_t)slot * (p.demux ? p.demux : 1u) : nullptr;
+        B.n = p.rg.n;
+        B.stride = p.rg.stride;
+        B.data_off = p.rg.data_off;
+        B.ntiles = p.uniform_ntiles;
+        *look_off = b * p.uniform_ntiles;
+    } else {
+        B = p.b[b];
+        *look_off = p.look_begin[b];
+    }
+    return B;
+}
+
+// Batch of global tile g: by division when every batch has the same tile
+// count, else a scalar scan of tile_begin[].
+__device__ __forceinline__ uint32_t batch_of_tile(const CopKParams &p, uint32_t g)
+{
+    uint32_t b = 0;
+    if (p.uniform_ntiles) {
+        b = g / p.uniform_ntiles;
+    } else {
+#pragma unroll
+        for (int q = 1; q < COPK_MAXB; q++) b += (q < (int)p.nb && p.tile_begin[q] <= g) ? 1u : 0u;
+    }
+    return __builtin_amdgcn_readfirstlane(b);
+}
+
+// Coalesced header loads of 64 consecutive packets (one "step" of a wave):
+// three 16-byte non-temporal loads per lane move the first 48 bytes of the
+// 64 packets; load c of lane l holds chunk (64c+l) mod 3 of packet
+// (64c+l)/3, so each load instruction covers about 1 KiB of contiguous slot
+// bytes (64-byte slots). StepGeom holds the per-lane constants.
+struct StepGeom {
+    uint32_t lpk[3], lch[3];   // packet (0..63) and chunk byte offset of load c
+    uint32_t r3;               // lane % 3
+    int a3, a67, a8;           // ds_bpermute byte addresses of this lane's sources
+};
+
+__device__ __forceinline__ StepGeom step_geom(int lane)
+{
+    StepGeom g;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const uint32_t q = (uint32_t)(c * 64 + lane);
+        g.lpk[c] = q / 3u;
+        g.lch[c] = (q % 3u) * 16u;
+    }
+    g.r3 = (uint32_t)lane % 3u;
+    g.a3 = ((3 * lane) & 63) << 2;
+    g.a67 = ((3 * lane + 1) & 63) << 2;
+    g.a8 = ((3 * lane + 2) & 63) << 2;
+    return g;
+}
+
+// the three loads of the step starting at packet pb (clamped to `last`)
+__device__ __forceinline__ void load_step(const StepGeom &g, const uint8_t *pk0, uint32_t stride, uint32_t pb,
+                                          uint32_t last, u32x4 (&v)[3])
+{
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const uint32_t ic = min(pb + g.lpk[c], last);
+        v[c] = __builtin_nontemporal_load((const u32x4 *)(pk0 + (size_t)ic * stride + g.lch[c]));
+    }
+}
+
+// The fields of this lane's packet (bytes 12..15 and 24..35) from the step's
+// loads: source lane s holds chunk k of its packet in load (k - s) mod 3, so
+// each field is one select at the source plus one ds_bpermute.
+__device__ __forceinline__ void gather_step(const StepGeom &g, const u32x4 (&v)[3], uint32_t &w3, uint32_t &w6,
+                                            uint32_t &w7, uint32_t &w8)
+{
+    const uint32_t c0w = g.r3 == 0 ? v[0].w : g.r3 == 1 ? v[2].w : v[1].w;
+    const uint32_t c1z = g.r3 == 0 ? v[1].z : g.r3 == 1 ? v[0].z : v[2].z;
+    const uint32_t c1w = g.r3 == 0 ? v[1].w : g.r3 == 1 ? v[0].w : v[2].w;
+    const uint32_t c2x = g.r3 == 0 ? v[2].x : g.r3 == 1 ? v[1].x : v[0].x;
+    w3 = (uint32_t)__builtin_amdgcn_ds_bpermute(g.a3, (int)c0w);
+    w6 = (uint32_t)__builtin_amdgcn_ds_bpermute(g.a67, (int)c1z);
+    w7 = (uint32_t)__builtin_amdgcn_ds_bpermute(g.a67, (int)c1w);
+    w8 = (uint32_t)__builtin_amdgcn_ds_bpermute(g.a8, (int)c2x);
+}
+
+// LDS views of the tables (staged at workgroup start)
+struct Tables {
+    const uint32_t *rt_top;
+    const uint16_t *rt_leaf;
+    const uint32_t *fw_s, *fw_v, *lp_s, *lp_v;
+};
+
+// Pass 1, per step: parse, vport route (stage P), interval searches in LDS,
+// and the tbl24 loads of DIR-24-8 stages (issued, not waited for).
+// w3 = bytes 12..15, w6/w7/w8 = bytes 24..35 of the packet as loaded (LE).
+template <int FW, int LPM, int PPT>
+__device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, const uint32_t (&w3)[PPT],
+                                      const uint32_t (&w6)[PPT], const uint32_t (&w7)[PPT],
+                                      const uint32_t (&w8)[PPT], uint32_t (&verdict)[PPT], uint32_t (&port)[PPT],
+                                      uint32_t (&src)[PPT], uint32_t (&dst)[PPT], uint32_t (&fwe)[PPT],
+                                      uint32_t (&lpe)[PPT])
+{
+    const bool stageP = (p.stages & COPK_STAGE_PARSE) != 0;
+    const uint32_t fw_lv = p.fw_m ? (uint32_t)__builtin_ctz(p.fw_m) : 0u;
+    const uint32_t lp_lv = p.lpm_m ? (uint32_t)__builtin_ctz(p.lpm_m) : 0u;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        verdict[k] = COPK_FORWARD;
+        port[k] = 0;
+        const uint32_t et = ((w3[k] & 0xFFu) << 8) | ((w3[k] >> 8) & 0xFFu);
+        dst[k] = bswap32(__builtin_amdgcn_alignbit(w8[k], w7[k], 16));
+        src[k] = bswap32(__builtin_amdgcn_alignbit(w7[k], w6[k], 16));
+        if (stageP) {
+            if (et != 0x0800u) {
+                verdict[k] = COPK_DROP_PARSE;
+                port[k] = 0xFFFFu;
+            } else {
+                const uint32_t idx = dst[k] & 0xFFFFu;
+                const uint32_t top = t.rt_top[idx >> 8];
+                port[k] = (top & 0x80000000u) ? (uint32_t)t.rt_leaf[((top & 0xFFFFu) << 8) | (idx & 0xFFu)]
+                                              : (top & 0xFFFFu);
+                if (port[k] == 0xFFFFu) verdict[k] = COPK_DROP_PARSE;
+                else if (port[k] >= p.n_ports) verdict[k] = COPK_DROP_NO_PORT;
+            }
+        }
+        if (FW == COPK_TBL_IVT) fwe[k] = t.fw_v[eyt_search(t.fw_s, fw_lv, src[k])];
+        if (FW == COPK_TBL_DIR) fwe[k] = p.fw_tbl24[src[k] >> 8];
+        if (LPM == COPK_TBL_IVT) lpe[k] = t.lp_v[eyt_search(t.lp_s, lp_lv, dst[k])];
+        if (LPM == COPK_TBL_DIR) lpe[k] = p.lpm_tbl24[dst[k] >> 8];
+    }
+}
+
+// Pass 2: rte_lpm_lookup's tbl8 step for valid+extended entries, then the
+// verdicts of stage FW (firewall.c:183-210) and stage LPM. Packets that did
+// not reach the coprocessor (stage P drop) keep their verdict. Counts the
+// FW stage's pkt_total / pkt_not_ipv4 (firewall.h:56-61) over valid packets.
+template <int FW, int LPM, int PPT>
+__device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[PPT], const uint32_t (&src)[PPT],
+                                      const uint32_t (&dst)[PPT], const bool (&valid)[PPT], uint32_t (&fwe)[PPT],
+                                      uint32_t (&lpe)[PPT], uint32_t (&verdict)[PPT], uint32_t (&flags)[PPT],
+                                      uint32_t (&rnh)[PPT], uint32_t &c_total, uint32_t &c_notv4)
+{
+    bool reached[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        reached[k] = verdict[k] == COPK_FORWARD;   // entered the coprocessor
+        flags[k] = 0;
+        rnh[k] = 0;
+    }
+    if (FW == COPK_TBL_DIR) {
+#pragma unroll
+        for (int k = 0; k < PPT; k++)
+            if ((fwe[k] & 0x03000000u) == 0x03000000u)
+                fwe[k] = p.fw_tbl8[((size_t)(fwe[k] & 0x00FFFFFFu) << 8) | (src[k] & 0xFFu)];
+    }
+    if (LPM == COPK_TBL_DIR) {
+#pragma unroll
+        for (int k = 0; k < PPT; k++)
+            if ((lpe[k] & 0x03000000u) == 0x03000000u)
+                lpe[k] = p.lpm_tbl8[((size_t)(lpe[k] & 0x00FFFFFFu) << 8) | (dst[k] & 0xFFu)];
+    }
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        if (!reached[k]) continue;
+        if (FW != COPK_TBL_OFF) {
+            c_total += valid[k];
+            if (((w3[k] >> 20) & 0xFu) != 4u) {
+                verdict[k] = COPK_DROP_NOT_IPV4;
+                c_notv4 += valid[k];
+            } else {
+                // rule-id image: bit 24 hit, bit 26 = the matching rule's
+                // action is non-zero (switch(rule) at firewall.c:201-210)
+                flags[k] |= (fwe[k] >> 24) & 1u ? COPK_FLAG_FW_HIT : 0u;
+                verdict[k] = (fwe[k] >> 26) & 1u ? COPK_DROP_FW : COPK_FORWARD;
+            }
+        }
+        if (LPM != COPK_TBL_OFF) {
+            flags[k] |= (lpe[k] >> 24) & 1u ? COPK_FLAG_ROUTE_HIT : 0u;
+            rnh[k] = lpe[k] & 0x00FFFFFFu;
+        }
+    }
+}
+
+// Per-rule hit counters: one relaxed device-scope u64 add per FW-stage hit
+// (no return value: fire-and-forget atomics at the L2/fabric).
+template <int FW, int PPT>
+__device__ __forceinline__ void rule_hit_atomics(const CopKParams &p, const bool (&valid)[PPT],
+                                                 const uint32_t (&flags)[PPT], const uint32_t (&fwe)[PPT])
+{
+    if (FW != COPK_TBL_OFF && p.rule_hits) {
+#pragma unroll
+        for (int k = 0; k < PPT; k++)
+            if (valid[k] && (flags[k] & COPK_FLAG_FW_HIT))
+                __hip_atomic_fetch_add(&p.rule_hits[fwe[k] & 0x00FFFFFFu], 1ull, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Result records (8 B per packet, coalesced, non-temporal: read by the host
+// or the next stage, never by this kernel) and the per-lane verdict counts.
+struct Counts {
+    uint32_t total = 0, notv4 = 0, fwd = 0, dropfw = 0, parse = 0, noport = 0, rhit = 0, rx = 0;
+};
+
+template <int PPT>
+__device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base, int tid, const bool (&valid)[PPT],
+                                              const uint32_t (&verdict)[PPT], const uint32_t (&flags)[PPT],
+                                              const uint32_t (&port)[PPT], const uint32_t (&rnh)[PPT],
+                                              bool (&fwd)[PPT], Counts &c)
+{
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        fwd[k] = valid[k] && verdict[k] == COPK_FORWARD;
+        if (valid[k]) {
+            u32x2 rec;
+            rec.x = verdict[k] | (flags[k] << 8) | (port[k] << 16);
+            rec.y = rnh[k];
+            __builtin_nontemporal_store(rec, &((u32x2 *)B.results)[base + k * BLOCK + tid]);
+            c.rx++;
+            c.fwd += verdict[k] == COPK_FORWARD;
+            c.dropfw += verdict[k] == COPK_DROP_FW;
+            c.parse += verdict[k] == COPK_DROP_PARSE;
+            c.noport += verdict[k] == COPK_DROP_NO_PORT;
+            c.rhit += flags[k] & COPK_FLAG_ROUTE_HIT;
+        }
+    }
+}
+
+// LDS scratch of one compaction: per-(step, wave) counts and the prefix of
+// the single-list form, or per-port counts and prefixes with demux.
+struct CompactLds {
+    volatile uint32_t *cnt;    // [PPT*WAVES]
+    volatile uint32_t *pref;   // [1]
+    volatile uint32_t *dq;     // [COPK_MAX_DEMUX_PORTS][PPT*WAVES]
+    volatile uint32_t *dpref;  // [COPK_MAX_DEMUX_PORTS]
+    uint32_t *stage;           // [BLOCK*PPT] the tile's forward list (single-list form) or nullptr
+};
+
+// Ordered compaction of one tile (packets base + k*BLOCK + tid): the
+// forward list of the batch, or one list per vport with demux (the tx_q
+// order of each port's coprocessor, switch.c:306-327 + 464-470; port q's
+// list at fwd_idx + q*n, its length at fwd_count[q]). Tile-local ballots and
+// an LDS scan over (step, wave), then decoupled look-back over the tiles of
+// the batch (one chain per port with demux, spread over the waves).
+// Contains two workgroup barriers; lb_off = the batch's first granule.
+// mid() runs between the look-back and the second barrier: the caller's
+// record stores go there, so the look-back's loads (vmcnt retires in order)
+// do not wait for them and the other waves store while wave 0 looks back.
+template <int PPT, typename Mid>
+__device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatch &B, uint32_t lb_off, uint32_t j,
+                                             uint32_t base, const bool (&fwd)[PPT], const uint32_t (&port)[PPT],
+                                             const CompactLds &s, int tid, int lane, int wave, Mid mid)
+{
+    constexpr int NQ = PPT * WAVES;
+    if (!p.demux) {
+        unsigned long long bal[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            bal[k] = __ballot(fwd[k]);
+            if (lane == 0) s.cnt[k * WAVES + wave] = (uint32_t)__popcll(bal[k]);
+        }
+        __syncthreads();
+        // every wave scans the tile's (step, wave) counts for its own offsets
+        uint32_t agg;
+        const uint32_t ex = wave_excl_scan(lane < NQ ? s.cnt[lane] : 0u, NQ, lane, &agg);
+        uint32_t off[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) off[k] = (uint32_t)__shfl((int)ex, k * WAVES + wave);
+        const bool staged = s.stage != nullptr && B.fwd_idx && !(p.dbg & 64u);
+        if (staged) {
+            // the tile's list in LDS, in order, while wave 0 looks back
+#pragma unroll
+            for (int k = 0; k < PPT; k++)
+                if (fwd[k])
+                    s.stage[off[k] + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[k] >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u))] =
+                        base + k * BLOCK + tid;
+        }
+        if (wave == 0) {
+            // dbg bit 32 (timing-only ablation): no look-back wait, wrong offsets
+            const uint32_t excl =
+                (p.dbg & 32u) ? j * 1024u : look_back(p.look + lb_off, 1u, j, agg, p.epoch, p.err, lane);
+            if (lane == 0) {
+                *s.pref = excl;
+                if (B.fwd_count && j == B.ntiles - 1) *B.fwd_count = excl + agg;
+            }
+        }
+        mid();
+        __syncthreads();
+        const uint32_t pref = *s.pref;
+        if (staged) {
+            // copy out in 16-byte stores on 16-byte boundaries of the list
+            // (partial words only at the tile's two ends)
+            const int mis = (int)(((uintptr_t)B.fwd_idx >> 2) & 3u);
+            const long a0 = (long)(((pref + (uint32_t)mis) & ~3u)) - mis;
+            const long end = (long)pref + agg;
+            const uint32_t nch = (uint32_t)((end - a0 + 3) / 4);
+            for (uint32_t c = (uint32_t)tid; c < nch; c += BLOCK) {
+                const long w0 = a0 + 4 * (long)c;
+                if (w0 >= (long)pref && w0 + 4 <= end) {
+                    const uint32_t i = (uint32_t)(w0 - (long)pref);
+                    u32x4 v;
+                    v.x = s.stage[i];
+                    v.y = s.stage[i + 1];
+                    v.z = s.stage[i + 2];
+                    v.w = s.stage[i + 3];
+                    __builtin_nontemporal_store(v, (u32x4 *)&B.fwd_idx[w0]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        const long w = w0 + i;
+                        if (w >= (long)pref && w < end)
+                            __builtin_nontemporal_store(s.stage[w - (long)pref], &B.fwd_idx[w]);
+                    }
+                }
+            }
+        } else if (B.fwd_idx && !(p.dbg & 64u)) {
+#pragma unroll
+            for (int k = 0; k < PPT; k++) {
+                if (fwd[k]) {
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi(
+                        (uint32_t)(bal[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u));
+                    __builtin_nontemporal_store(base + k * BLOCK + tid, &B.fwd_idx[pref + off[k] + r]);
+                }
+            }
+        }
+        return;
+    }
+    const uint32_t K = p.demux;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        for (uint32_t q = 0; q < K; q++) {
+            const unsigned long long b = __ballot(fwd[k] && port[k] == q);
+            if (lane == 0) s.dq[q * NQ + k * WAVES + wave] = (uint32_t)__popcll(b);
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = (uint32_t)wave; q < K; q += WAVES) {
+        uint32_t agg;
+        const uint32_t ex = wave_excl_scan(lane < NQ ? s.dq[q * NQ + lane] : 0u, NQ, lane, &agg);
+        if (lane < NQ) s.dq[q * NQ + lane] = ex;
+        const uint32_t excl = look_back(p.look + (size_t)lb_off * K + q, K, j, agg, p.epoch, p.err, lane);
+        if (lane == 0) {
+            s.dpref[q] = excl;
+            if (B.fwd_count && j == B.ntiles - 1) B.fwd_count[q] = excl + agg;
+        }
+    }
+    mid();
+    __syncthreads();
+    if (B.fwd_idx) {
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            uint32_t r = 0;
+            for (uint32_t q = 0; q < K; q++) {
+                const bool mine = fwd[k] && port[k] == q;
+                const unsigned long long b = __ballot(mine);
+                if (mine)
+                    r = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            }
+            if (fwd[k]) {
+                const uint32_t q = port[k];
+                __builtin_nontemporal_store(
+                    base + k * BLOCK + tid, &B.fwd_idx[(size_t)q * B.n + s.dpref[q] + s.dq[q * NQ + k * WAVES + wave] + r]);
+            }
+        }
+    }
+}
+
+// Per-port coprocessor_stats (switch.h:33-38) of one tile, added to
+// wave-uniform accumulators: rx = packets routed to the port's NF
+// (enqueue_nf_rx), tx = packets it forwarded.
+template <int PPT>
+__device__ __forceinline__ void port_counts(uint32_t K, const bool (&valid)[PPT], const bool (&fwd)[PPT],
+                                            const uint32_t (&port)[PPT], uint32_t (&prx)[COPK_MAX_DEMUX_PORTS],
+                                            uint32_t (&ptx)[COPK_MAX_DEMUX_PORTS])
+{
+#pragma unroll
+    for (int q = 0; q < COPK_MAX_DEMUX_PORTS; q++) {
+        if ((uint32_t)q >= K) break;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            prx[q] += (uint32_t)__popcll(__ballot(valid[k] && port[k] == (uint32_t)q));
+            ptx[q] += (uint32_t)__popcll(__ballot(fwd[k] && port[k] == (uint32_t)q));
+        }
+    }
+}
+
+// Workgroup counter flush: wave reduce -> LDS -> one atomic per counter per
+// workgroup, into one of COPK_COUNTER_SHARDS shards (a 128-byte line each)
+// so no single word serialises thousands of atomics; then the per-port
+// counters the same way. s_red: WAVES*8 words, s_ps: WAVES*16 words.
+__device__ __forceinline__ void flush_counters(const CopKParams &p, const Counts &cn,
+                                               const uint32_t (&prx)[COPK_MAX_DEMUX_PORTS],
+                                               const uint32_t (&ptx)[COPK_MAX_DEMUX_PORTS], uint32_t *s_red,
+                                               volatile uint32_t *s_ps, int tid, int lane, int wave)
+{
+    uint32_t c[8] = {cn.total, cn.notv4, cn.fwd, cn.dropfw, cn.parse, cn.noport, cn.rhit, cn.rx};
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        uint32_t v = c[q];
+#pragma unroll
+        for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off);
+        c[q] = v;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) s_red[wave * 8 + q] = c[q];
+    }
+    const uint32_t K = p.port_stats;
+    if (K && lane == 0) {
+#pragma unroll
+        for (int q = 0; q < COPK_MAX_DEMUX_PORTS; q++) {
+            if ((uint32_t)q >= K) break;
+            s_ps[wave * 16 + 2 * q] = prx[q];
+            s_ps[wave * 16 + 2 * q + 1] = ptx[q];
+        }
+    }
+    __syncthreads();
+    if (tid < 9) {
+        uint32_t r[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int w = 0; w < WAVES; w++) v += s_red[w * 8 + q];
+            r[q] = v;
+        }
+        // cop_counters order: drop, accept, not_ipv4, total, parse_err, no_port, forward, route_hit, rx
+        uint32_t v;
+        switch (tid) {
+        case 0: v = r[3] + r[1]; break;
+        case 1: v = r[0] - r[1] - r[3]; break;
+        case 2: v = r[1]; break;
+        case 3: v = r[0]; break;
+        case 4: v = r[4]; break;
+        case 5: v = r[5]; break;
+        case 6: v = r[2]; break;
+        case 7: v = r[6]; break;
+        default: v = r[7]; break;
+        }
+        if (v && !(p.dbg & 1u))
+            atomicAdd(&p.counters[(blockIdx.x % COPK_COUNTER_SHARDS) * 16 + tid], (unsigned long long)v);
+    }
+    if (K && tid < 2 * K) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; w++) v += s_ps[w * 16 + tid];
+        if (v)
+            atomicAdd(&p.port_ctr[(blockIdx.x % COPK_COUNTER_SHARDS) * COPK_PORT_WORDS + tid], (unsigned long long)v);
+    }
+}
+
+}  // namespace copd
+
+#endif

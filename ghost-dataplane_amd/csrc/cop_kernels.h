@@ -13,6 +13,8 @@
 static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_LDS_MISC_WORDS 80       /* counts, tile, prefix, counter reduction */
 #define COPK_LDS_MISC_EXT_WORDS 408  /* + per-port counts/prefixes (demux, port stats) */
+#define COPK_LDS_STREAM_MISC_WORDS 608  /* stream kernel: counter reduction, port stats, tile counts */
+#define COPK_STREAM_MIN_STRIDE 48    /* the stream kernel reads the first 48 bytes of a packet */
 #define COPK_MAX_DEMUX_PORTS 8
 #define COPK_PORT_WORDS 16           /* per shard: 8 ports x {rx, tx} */
 #define COPK_STAMP_WG 65536
@@ -20,6 +22,10 @@ static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_TBL_OFF 0
 #define COPK_TBL_IVT 1  /* flattened intervals, binary search in LDS */
 #define COPK_TBL_DIR 2  /* DIR-24-8 image in HBM */
+
+#define COPK_LAY_SLOTS 0      /* packet layouts of the one-shot kernel */
+#define COPK_LAY_IMIX 1
+#define COPK_LAY_COALESCED 2
 
 #define COPK_STAGE_PARSE 0x1u
 
@@ -81,6 +87,7 @@ struct CopKParams {
     const uint32_t *lpm_tbl24, *lpm_tbl8;
     // LDS carve (u32 words)
     uint32_t lds_fw_off, lds_lpm_off, lds_misc_off;
+    uint32_t lds_stage_off;   // one-shot kernel: the tile's forward list staged in LDS (0: none)
     // ordering / accounting state
     unsigned long long *tickets;   // one counter per batch, one 128-byte line each (zero at launch)
     unsigned long long *zero_tickets;  // the lane's other ticket buffer: zeroed by this launch
@@ -98,8 +105,14 @@ struct CopKParams {
 #ifdef __cplusplus
 extern "C" {
 #endif
-hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int imix, int ppt,
+// layout: COPK_LAY_*
+hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int layout, int ppt,
                        uint32_t grid, uint32_t lds_bytes, hipStream_t stream);
+// persistent batch-sweep kernel (cop_stream.hip): grid <= co-resident
+// workgroups and <= p->nb; one workgroup per batch at a time
+hipError_t copk_launch_stream(const CopKParams *p, int fw_mode, int lpm_mode, int ppt, uint32_t grid,
+                              uint32_t lds_bytes, hipStream_t stream);
+hipError_t copk_stream_occupancy(int fw_mode, int lpm_mode, int ppt, uint32_t lds_bytes, int *blocks_per_cu);
 // dst[i] = src[i] (atomic load) or atomic exchange with 0 when reset
 hipError_t copk_snapshot(unsigned long long *src, uint32_t n_words, unsigned long long *dst, int reset,
                          hipStream_t stream);

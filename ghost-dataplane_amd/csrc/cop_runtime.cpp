@@ -16,6 +16,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -152,6 +153,13 @@ struct cop_ctx {
     cop_config cfg{};
     int ncu = 256;
     int ppt_override = 0;      // $COP_PPT (1, 4, 8) for experiments; 0 = auto
+    int kernel_mode = COP_KERNEL_AUTO;   // cop_set_kernel_mode / $COP_KERNEL
+    int stream_ppt = 4;        // streaming kernel tile = 256 * stream_ppt ($COP_STREAM_PPT 1, 2, 4)
+    int stream_occ = 2;        // streaming kernel workgroups per CU, at most ($COP_STREAM_OCC)
+    uint32_t stream_min_batches = 0xFFFFFFFFu;   // auto: batch-sweep kernel from this many batches (off; $COP_STREAM_MIN_BATCHES)
+    int occ_key = -1, occ_val = 0;   // cached occupancy query
+    bool coalesced = true;     // one-shot kernel: coalesced header loads where eligible ($COP_LOADS=strided: off)
+    bool stage_lists = true;   // one-shot kernel: forward lists staged in LDS ($COP_STAGE_LISTS=0: off)
     uint32_t dbg = 0;          // $COP_DBG: timing-only kernel ablations
     unsigned long long *stamps = nullptr;   // dbg bit 8: per-workgroup phase stamps
     char err[256] = {0};
@@ -388,6 +396,21 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
         c->ppt_override = (v == 1 || v == 4 || v == 8) ? v : 0;
     }
     if (const char *e = getenv("COP_DBG")) c->dbg = (uint32_t)strtoul(e, nullptr, 0);
+    if (const char *e = getenv("COP_KERNEL")) {
+        if (!strcmp(e, "oneshot")) c->kernel_mode = COP_KERNEL_ONESHOT;
+        else if (!strcmp(e, "stream")) c->kernel_mode = COP_KERNEL_STREAM;
+    }
+    if (const char *e = getenv("COP_LOADS")) c->coalesced = strcmp(e, "strided") != 0;
+    if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
+    if (const char *e = getenv("COP_STREAM_PPT")) {
+        int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4) c->stream_ppt = v;
+    }
+    if (const char *e = getenv("COP_STREAM_MIN_BATCHES")) c->stream_min_batches = (uint32_t)strtoul(e, nullptr, 0);
+    if (const char *e = getenv("COP_STREAM_OCC")) {
+        int v = atoi(e);
+        if (v >= 1 && v <= 8) c->stream_occ = v;
+    }
     if (const char *e = getenv("COP_STREAMS")) {
         int v = atoi(e);
         if (v >= 1 && v <= MAX_LANES) cfg.n_streams = (uint32_t)v;
@@ -604,16 +627,42 @@ static int choose_ppt(const cop_ctx *c, uint64_t total)
     return ppt;
 }
 
+// Which kernel runs a launch, and its tile size (256 * ppt packets).
+struct Plan {
+    bool stream;
+    int ppt;
+    int layout;   // one-shot kernel: COPK_LAY_*
+};
+
+static Plan plan_launch(const cop_ctx *c, uint64_t total, uint32_t nb, bool imix, uint32_t min_stride)
+{
+    const bool eligible = !imix && min_stride >= COPK_STREAM_MIN_STRIDE;
+    Plan pl{false, choose_ppt(c, total),
+            imix ? COPK_LAY_IMIX : (eligible && c->coalesced) ? COPK_LAY_COALESCED : COPK_LAY_SLOTS};
+    if (!eligible || c->kernel_mode == COP_KERNEL_ONESHOT) return pl;
+    // the batch-sweep kernel runs one workgroup per batch: worth it when
+    // there are batches for every CU and each is many tiles long
+    const uint64_t per_batch = nb ? total / nb : 0;
+    if (c->kernel_mode == COP_KERNEL_STREAM ||
+        (nb >= c->stream_min_batches && per_batch >= 16ull * COPK_BLOCK * (uint64_t)c->stream_ppt)) {
+        pl.stream = true;
+        pl.ppt = c->stream_ppt;
+    }
+    return pl;
+}
+
 // Fill the table / state part of the parameters and launch on lane L.
 // p.b / p.rg, p.nb, p.ntiles, p.uniform_ntiles and p.compact are set by the caller.
-static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, int ppt, uint32_t nb_used)
+static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uint32_t nb_used)
 {
+    const int ppt = pl.ppt;
     const uint32_t stages = c->cfg.stages;
     int fw_mode = pick_mode(c, c->fw, (stages & COP_STAGE_FW) != 0, (c->cfg.flags & COP_CFG_FW_FORCE_DIR24) != 0);
     int lpm_mode =
         pick_mode(c, c->lpm, (stages & COP_STAGE_LPM) != 0, (c->cfg.flags & COP_CFG_LPM_FORCE_DIR24) != 0);
     HIPCHK(c, hipSetDevice(c->device));
-    const uint32_t look_need = p.ntiles * (p.demux ? p.demux : 1u);   // one chain per port (demux)
+    // one chain per port (demux); the batch-sweep kernel needs none
+    const uint32_t look_need = pl.stream ? 0u : p.ntiles * (p.demux ? p.demux : 1u);
     if (look_need > L.look_cap) {
         // grow this lane's look-back words (stream order: free after its work)
         HIPCHK(c, hipStreamSynchronize(L.s));
@@ -653,7 +702,13 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, int ppt, uin
     p.lds_lpm_off = off;
     off += 2 * p.lpm_m;
     p.lds_misc_off = off;
-    off += (p.demux || (c->cfg.flags & COP_CFG_PORT_STATS)) ? COPK_LDS_MISC_EXT_WORDS : COPK_LDS_MISC_WORDS;
+    if (pl.stream) off += COPK_LDS_STREAM_MISC_WORDS;
+    else off += (p.demux || (c->cfg.flags & COP_CFG_PORT_STATS)) ? COPK_LDS_MISC_EXT_WORDS : COPK_LDS_MISC_WORDS;
+    p.lds_stage_off = 0;
+    if (!pl.stream && p.compact && !p.demux && c->stage_lists) {
+        p.lds_stage_off = off;   // the tile's forward list, written out in 16-byte stores
+        off += COPK_BLOCK * ppt;
+    }
     const uint32_t lds_bytes = off * 4;
     if (lds_bytes > 160 * 1024) return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_bytes);
     // tickets: draw from buffer `parity`, zero the other buffer's dirty lines
@@ -669,16 +724,32 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, int ppt, uin
     p.err = c->d_err;
     p.stamps = c->stamps;
     if ((c->dbg & 8u) && p.ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
-    const uint32_t grid = p.ntiles;   // one tile per workgroup
+    uint32_t grid = p.ntiles;   // one-shot: one tile per workgroup
+    if (pl.stream) {
+        // persistent: no more workgroups than are co-resident (the static
+        // tile order's look-back relies on it), at most stream_occ per CU
+        const int key = ((fw_mode * 4 + lpm_mode) * 8 + ppt) * (160 * 1024 + 1) + (int)lds_bytes;
+        if (key != c->occ_key) {
+            int occ = 0;
+            hipError_t oe = copk_stream_occupancy(fw_mode, lpm_mode, ppt, lds_bytes, &occ);
+            if (oe != hipSuccess || occ < 1)
+                return set_err(c, -EIO, "stream kernel occupancy: %s (%d)", hipGetErrorString(oe), occ);
+            c->occ_key = key;
+            c->occ_val = occ;
+        }
+        const uint64_t resident = (uint64_t)c->ncu * (uint64_t)std::min(c->occ_val, c->stream_occ);
+        grid = (uint32_t)std::min<uint64_t>(p.nb, resident);   // one workgroup per batch at a time
+    }
 
     if (c->timing) {
         if (L.ev_count == TIMING_SLOTS) harvest_one(c, L);
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][0], L.s));
     }
-    hipError_t e = copk_launch(&p, fw_mode, lpm_mode, imix ? 1 : 0, ppt, grid, lds_bytes, L.s);
+    hipError_t e = pl.stream ? copk_launch_stream(&p, fw_mode, lpm_mode, ppt, grid, lds_bytes, L.s)
+                             : copk_launch(&p, fw_mode, lpm_mode, pl.layout, ppt, grid, lds_bytes, L.s);
     if (e != hipSuccess) return set_err(c, -EIO, "launch: %s", hipGetErrorString(e));
     L.dirty[q ^ 1] = 0;
-    L.dirty[q] = (p.compact && !(c->dbg & 2u)) ? nb_used : 0;
+    L.dirty[q] = (p.compact && !(c->dbg & 2u) && !pl.stream) ? nb_used : 0;
     L.parity = q ^ 1;
     if (c->timing) {
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][1], L.s));
@@ -712,8 +783,11 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb,
         if (b.fwd_idx || b.fwd_count) compact = true;
     }
     if (c->cfg.flags & COP_CFG_NO_COMPACT) compact = false;
-    const int ppt = choose_ppt(c, total);
-    const uint32_t tile = COPK_BLOCK * ppt;
+    uint32_t min_stride = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < nb; i++)
+        if (batches[i].n) min_stride = std::min(min_stride, batches[i].stride);
+    const Plan pl = plan_launch(c, total, nb, imix, min_stride);
+    const uint32_t tile = COPK_BLOCK * pl.ppt;
     uint32_t ntiles = 0;
     for (uint32_t i = 0; i < nb; i++) {
         const cop_batch &b = batches[i];
@@ -739,7 +813,7 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb,
         if (p.b[i].ntiles != p.b[0].ntiles) p.uniform_ntiles = 0;
     p.compact = compact ? 1u : 0u;
     p.demux = (demux && compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 0u;
-    return launch_on(c, L, p, imix, ppt, nb);
+    return launch_on(c, L, p, imix, pl, nb);
 }
 
 int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, uint32_t count)
@@ -758,8 +832,8 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     const uint32_t lists = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 1u;
     if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < (uint64_t)r->n * lists))
         return set_err(c, -EINVAL, "ring: slot sizes smaller than n (x ports with demux)");
-    const int ppt = choose_ppt(c, (uint64_t)r->n * count);
-    const uint32_t tile = COPK_BLOCK * ppt;
+    const Plan pl = plan_launch(c, (uint64_t)r->n * count, count, imix, r->stride);
+    const uint32_t tile = COPK_BLOCK * pl.ppt;
     const uint32_t tpb = r->n ? (r->n + tile - 1) / tile : 1;
     CopKParams p;
     memset(&p, 0, sizeof(p));
@@ -785,7 +859,14 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     p.demux = lists > 1 || (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? lists : 0u;
     Lane &L = c->lane[c->next_lane];
     c->next_lane = (c->next_lane + 1) % c->n_lanes;
-    return launch_on(c, L, p, imix, ppt, count);
+    return launch_on(c, L, p, imix, pl, count);
+}
+
+int cop_set_kernel_mode(cop_ctx *c, int mode)
+{
+    if (!c || mode < COP_KERNEL_AUTO || mode > COP_KERNEL_STREAM) return -EINVAL;
+    c->kernel_mode = mode;
+    return 0;
 }
 
 int cop_sync(cop_ctx *c)

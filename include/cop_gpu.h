@@ -226,9 +226,10 @@ int  cop_load_fw_rules_file(cop_ctx *ctx, const char *path, const cop_lpm_config
 
 /* One batch of packets resident in device memory (HBM).
  * Packet i starts at  pkts + (offsets ? offsets[i] : i * stride) + data_off.
- * Every packet start must be 16-byte aligned and hold >= 34 readable bytes
- * (Ethernet + IPv4 header, fixed offsets as firewall.c:143-145 /
- * switch.c:125-127 read them). Outputs: results[i] for every packet;
+ * Every packet start must be 16-byte aligned and hold >= 48 readable bytes
+ * (the fields sit at fixed offsets 12..33, as firewall.c:143-145 /
+ * switch.c:125-127 read them; the streaming kernel moves whole 16-byte
+ * chunks, and any Ethernet frame has >= 60). Outputs: results[i] for every packet;
  * fwd_idx[0..*fwd_count) = indices of FORWARD packets in arrival order (the
  * order coprocessor() enqueues them to tx_q, switch.c:464-470). */
 typedef struct cop_batch {
@@ -296,6 +297,17 @@ int  cop_process_host_stream(cop_ctx *ctx, const void *const *pkt_data, uint64_t
 /* Host threads for the header gather of the two calls above: the calling
  * thread plus n-1 persistent workers (default 1 = the caller alone). */
 int  cop_set_host_threads(cop_ctx *ctx, uint32_t n);
+
+/* Kernel selection (tuning; results are identical either way):
+ * COP_KERNEL_AUTO (default) runs one workgroup per tile (the faster form at
+ * every measured shape); STREAM uses the persistent batch-sweep kernel (one
+ * workgroup sweeps a whole batch) whenever the launch is eligible (packet
+ * batches at stride >= 48, no IMIX offsets); ONESHOT never.
+ * Also $COP_KERNEL = auto | oneshot | stream. */
+#define COP_KERNEL_AUTO    0
+#define COP_KERNEL_ONESHOT 1
+#define COP_KERNEL_STREAM  2
+int  cop_set_kernel_mode(cop_ctx *ctx, int mode);
 
 /* Counters (u64, device-resident, summed over every submitted packet).
  * On the device they are kept in COP_COUNTER_SHARDS shards of
