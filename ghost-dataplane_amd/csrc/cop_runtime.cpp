@@ -161,6 +161,7 @@ struct cop_ctx {
     bool coalesced = true;     // one-shot kernel: coalesced header loads where eligible ($COP_LOADS=strided: off)
     bool stage_lists = true;   // one-shot kernel: forward lists staged in LDS ($COP_STAGE_LISTS=0: off)
     uint32_t dbg = 0;          // $COP_DBG: timing-only kernel ablations
+    uint32_t lds_pad = 0;      // $COP_LDS_PAD: extra LDS bytes per workgroup (occupancy experiments)
     unsigned long long *stamps = nullptr;   // dbg bit 8: per-workgroup phase stamps
     char err[256] = {0};
 
@@ -396,6 +397,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
         c->ppt_override = (v == 1 || v == 4 || v == 8) ? v : 0;
     }
     if (const char *e = getenv("COP_DBG")) c->dbg = (uint32_t)strtoul(e, nullptr, 0);
+    if (const char *e = getenv("COP_LDS_PAD")) c->lds_pad = (uint32_t)strtoul(e, nullptr, 0) & ~15u;
     if (const char *e = getenv("COP_KERNEL")) {
         if (!strcmp(e, "oneshot")) c->kernel_mode = COP_KERNEL_ONESHOT;
         else if (!strcmp(e, "stream")) c->kernel_mode = COP_KERNEL_STREAM;
@@ -709,7 +711,7 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
         p.lds_stage_off = off;   // the tile's forward list, written out in 16-byte stores
         off += COPK_BLOCK * ppt;
     }
-    const uint32_t lds_bytes = off * 4;
+    const uint32_t lds_bytes = off * 4 + c->lds_pad;
     if (lds_bytes > 160 * 1024) return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_bytes);
     // tickets: draw from buffer `parity`, zero the other buffer's dirty lines
     const int q = L.parity;

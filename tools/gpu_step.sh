@@ -4,6 +4,7 @@
 # are reported but do not stop later steps.
 # usage: tools/gpu_step.sh <seconds> <log> <cmd...>
 secs=$1; log=$2; shift 2
+mkdir -p "$(dirname "$log")"
 echo "=== $(date +%T) step: $* (limit ${secs}s) -> $log"
 timeout -k 10 "$secs" "$@" > "$log" 2>&1
 rc=$?
