@@ -38,6 +38,20 @@ __device__ __forceinline__ unsigned long long lb_load(unsigned long long *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Workgroup barrier that orders LDS only. __syncthreads() is a workgroup
+// fence plus s_barrier, and the fence waits for every outstanding global load
+// and store of the wave (vmcnt(0)): prefetched tiles and in-flight record
+// stores would drain at every barrier. Cross-workgroup data (look-back
+// granules, counters) is ordered by agent-scope atomics, not by barriers.
+// LDS-DMA (global_load_lds) completion is counted by vmcnt: wait for staged
+// tables with __syncthreads().
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ void lds_stage(uint32_t *lds_dst, const void *gsrc, uint32_t n16, int lane, int wave)
 {
     // one 1 KiB piece per wave-instruction: LDS destination = base + lane*16
@@ -427,13 +441,43 @@ __device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base,
     }
 }
 
+// Copy a tile's forward list (agg indices staged in LDS, in order) to
+// fwd_idx[pref ..]: 16-byte non-temporal stores on 16-byte boundaries of
+// the list, partial words only at the two ends. All BLOCK data threads.
+__device__ __forceinline__ void copy_out_list(uint32_t *fwd_idx, uint32_t pref, uint32_t agg, const uint32_t *stage,
+                                              int tid)
+{
+    const int mis = (int)(((uintptr_t)fwd_idx >> 2) & 3u);
+    const long a0 = (long)(((pref + (uint32_t)mis) & ~3u)) - mis;
+    const long end = (long)pref + agg;
+    const uint32_t nch = (uint32_t)((end - a0 + 3) / 4);
+    for (uint32_t c = (uint32_t)tid; c < nch; c += BLOCK) {
+        const long w0 = a0 + 4 * (long)c;
+        if (w0 >= (long)pref && w0 + 4 <= end) {
+            const uint32_t i = (uint32_t)(w0 - (long)pref);
+            u32x4 v;
+            v.x = stage[i];
+            v.y = stage[i + 1];
+            v.z = stage[i + 2];
+            v.w = stage[i + 3];
+            __builtin_nontemporal_store(v, (u32x4 *)&fwd_idx[w0]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const long w = w0 + i;
+                if (w >= (long)pref && w < end) __builtin_nontemporal_store(stage[w - (long)pref], &fwd_idx[w]);
+            }
+        }
+    }
+}
+
 // LDS scratch of one compaction: per-(step, wave) counts and the prefix of
 // the single-list form, or per-port counts and prefixes with demux.
 struct CompactLds {
-    volatile uint32_t *cnt;    // [PPT*WAVES]
-    volatile uint32_t *pref;   // [1]
-    volatile uint32_t *dq;     // [COPK_MAX_DEMUX_PORTS][PPT*WAVES]
-    volatile uint32_t *dpref;  // [COPK_MAX_DEMUX_PORTS]
+    uint32_t *cnt;    // [PPT*WAVES]
+    uint32_t *pref;   // [1]
+    uint32_t *dq;     // [COPK_MAX_DEMUX_PORTS][PPT*WAVES]
+    uint32_t *dpref;  // [COPK_MAX_DEMUX_PORTS]
     uint32_t *stage;           // [BLOCK*PPT] the tile's forward list (single-list form) or nullptr
 };
 
@@ -460,7 +504,7 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatc
             bal[k] = __ballot(fwd[k]);
             if (lane == 0) s.cnt[k * WAVES + wave] = (uint32_t)__popcll(bal[k]);
         }
-        __syncthreads();
+        lds_barrier();
         // every wave scans the tile's (step, wave) counts for its own offsets
         uint32_t agg;
         const uint32_t ex = wave_excl_scan(lane < NQ ? s.cnt[lane] : 0u, NQ, lane, &agg);
@@ -487,34 +531,10 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatc
             }
         }
         mid();
-        __syncthreads();
+        lds_barrier();
         const uint32_t pref = *s.pref;
         if (staged) {
-            // copy out in 16-byte stores on 16-byte boundaries of the list
-            // (partial words only at the tile's two ends)
-            const int mis = (int)(((uintptr_t)B.fwd_idx >> 2) & 3u);
-            const long a0 = (long)(((pref + (uint32_t)mis) & ~3u)) - mis;
-            const long end = (long)pref + agg;
-            const uint32_t nch = (uint32_t)((end - a0 + 3) / 4);
-            for (uint32_t c = (uint32_t)tid; c < nch; c += BLOCK) {
-                const long w0 = a0 + 4 * (long)c;
-                if (w0 >= (long)pref && w0 + 4 <= end) {
-                    const uint32_t i = (uint32_t)(w0 - (long)pref);
-                    u32x4 v;
-                    v.x = s.stage[i];
-                    v.y = s.stage[i + 1];
-                    v.z = s.stage[i + 2];
-                    v.w = s.stage[i + 3];
-                    __builtin_nontemporal_store(v, (u32x4 *)&B.fwd_idx[w0]);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; i++) {
-                        const long w = w0 + i;
-                        if (w >= (long)pref && w < end)
-                            __builtin_nontemporal_store(s.stage[w - (long)pref], &B.fwd_idx[w]);
-                    }
-                }
-            }
+            copy_out_list(B.fwd_idx, pref, agg, s.stage, tid);
         } else if (B.fwd_idx && !(p.dbg & 64u)) {
 #pragma unroll
             for (int k = 0; k < PPT; k++) {
@@ -535,7 +555,7 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatc
             if (lane == 0) s.dq[q * NQ + k * WAVES + wave] = (uint32_t)__popcll(b);
         }
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t q = (uint32_t)wave; q < K; q += WAVES) {
         uint32_t agg;
         const uint32_t ex = wave_excl_scan(lane < NQ ? s.dq[q * NQ + lane] : 0u, NQ, lane, &agg);
@@ -547,7 +567,7 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatc
         }
     }
     mid();
-    __syncthreads();
+    lds_barrier();
     if (B.fwd_idx) {
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
@@ -593,7 +613,7 @@ __device__ __forceinline__ void port_counts(uint32_t K, const bool (&valid)[PPT]
 __device__ __forceinline__ void flush_counters(const CopKParams &p, const Counts &cn,
                                                const uint32_t (&prx)[COPK_MAX_DEMUX_PORTS],
                                                const uint32_t (&ptx)[COPK_MAX_DEMUX_PORTS], uint32_t *s_red,
-                                               volatile uint32_t *s_ps, int tid, int lane, int wave)
+                                               uint32_t *s_ps, int tid, int lane, int wave)
 {
     uint32_t c[8] = {cn.total, cn.notv4, cn.fwd, cn.dropfw, cn.parse, cn.noport, cn.rhit, cn.rx};
 #pragma unroll
@@ -603,12 +623,12 @@ __device__ __forceinline__ void flush_counters(const CopKParams &p, const Counts
         for (int off = 32; off; off >>= 1) v += __shfl_xor(v, off);
         c[q] = v;
     }
-    if (lane == 0) {
+    if (lane == 0 && wave < WAVES) {   // (a coordinator wave beyond the data waves adds nothing)
 #pragma unroll
         for (int q = 0; q < 8; q++) s_red[wave * 8 + q] = c[q];
     }
     const uint32_t K = p.port_stats;
-    if (K && lane == 0) {
+    if (K && lane == 0 && wave < WAVES) {
 #pragma unroll
         for (int q = 0; q < COPK_MAX_DEMUX_PORTS; q++) {
             if ((uint32_t)q >= K) break;
@@ -616,7 +636,7 @@ __device__ __forceinline__ void flush_counters(const CopKParams &p, const Counts
             s_ps[wave * 16 + 2 * q + 1] = ptx[q];
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < 9) {
         uint32_t r[8];
 #pragma unroll

@@ -82,14 +82,14 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
     tb.lp_s = lp_s;
     tb.lp_v = lp_v;
     uint32_t *misc = lds + p.lds_misc_off;
-    volatile uint32_t *s_tile = misc + 32;
+    uint32_t *s_tile = misc + 32;
     uint32_t *s_red = misc + 40;                              // [WAVES][8]
     CompactLds cl;
     cl.cnt = misc;                                            // [PPT*WAVES]
     cl.pref = misc + 33;
     cl.dq = misc + COPK_LDS_MISC_WORDS;                       // [K][PPT*WAVES]
     cl.dpref = cl.dq + COPK_MAX_DEMUX_PORTS * PPT * WAVES;    // [K]
-    volatile uint32_t *s_ps = cl.dpref + 8;                   // [WAVES][16]
+    uint32_t *s_ps = cl.dpref + 8;                   // [WAVES][16]
     cl.stage = p.lds_stage_off ? lds + p.lds_stage_off : nullptr;   // [TILE]
 
     STAMP(0);

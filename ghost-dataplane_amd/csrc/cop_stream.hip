@@ -161,7 +161,7 @@ __global__ __launch_bounds__(BLOCK, 2) void cop_stream(const CopKParams p)
         // ---- ordered compaction: tile-local ballots + LDS scan, appended
         // at the batch's running list lengths ----
         if (p.compact) {
-            volatile uint32_t *cnt = misc + SM_CNT + par * (COPK_MAX_DEMUX_PORTS * 32);
+            uint32_t *cnt = misc + SM_CNT + par * (COPK_MAX_DEMUX_PORTS * 32);
 #pragma unroll
             for (int q = 0; q < COPK_MAX_DEMUX_PORTS; q++) {
                 if ((uint32_t)q >= K) break;
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(BLOCK, 2) void cop_stream(const CopKParams p)
                     if (lane == 0) cnt[q * 32 + k * WAVES + wave] = (uint32_t)__popcll(bl);
                 }
             }
-            __syncthreads();
+            lds_barrier();
             uint32_t off[PPT] = {};
 #pragma unroll
             for (int q = 0; q < COPK_MAX_DEMUX_PORTS; q++) {
