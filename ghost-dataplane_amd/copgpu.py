@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(HERE, "libcopgpu.so")
 
 # ---------------------------------------------------------------------------
 # constants (include/cop_gpu.h)
-KERNEL_AUTO, KERNEL_ONESHOT, KERNEL_STREAM, KERNEL_SWEEP = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_ONESHOT, KERNEL_STREAM = 0, 1, 2
 STAGE_PARSE, STAGE_FW, STAGE_LPM = 0x1, 0x2, 0x4
 FORWARD, DROP_FW, DROP_PARSE, DROP_NOT_IPV4, DROP_NO_PORT = 0, 1, 2, 3, 4
 FLAG_ROUTE_HIT, FLAG_FW_HIT = 0x1, 0x2
@@ -515,7 +515,7 @@ class Context:
         _check(lib().cop_set_host_threads(self.handle, n), self, "set_host_threads")
 
     def set_kernel_mode(self, mode: int):
-        """KERNEL_AUTO, KERNEL_ONESHOT, KERNEL_STREAM or KERNEL_SWEEP (identical results)."""
+        """KERNEL_AUTO, KERNEL_ONESHOT or KERNEL_STREAM (identical results)."""
         _check(lib().cop_set_kernel_mode(self.handle, mode), self, "set_kernel_mode")
 
     def process_host_stream(self, ptrs: np.ndarray, batch: int) -> np.ndarray:

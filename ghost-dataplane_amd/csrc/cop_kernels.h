@@ -14,7 +14,6 @@ static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_LDS_MISC_WORDS 80       /* counts, tile, prefix, counter reduction */
 #define COPK_LDS_MISC_EXT_WORDS 408  /* + per-port counts/prefixes (demux, port stats) */
 #define COPK_LDS_STREAM_MISC_WORDS 608  /* stream kernel: counter reduction, port stats, tile counts */
-#define COPK_LDS_SWEEP_MISC_WORDS 176  /* sweep kernel: tile queue, prefixes, counts, counter reduction */
 #define COPK_STREAM_MIN_STRIDE 48    /* the stream kernel reads the first 48 bytes of a packet */
 #define COPK_MAX_DEMUX_PORTS 8
 #define COPK_PORT_WORDS 16           /* per shard: 8 ports x {rx, tx} */
@@ -114,12 +113,6 @@ hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int layou
 hipError_t copk_launch_stream(const CopKParams *p, int fw_mode, int lpm_mode, int ppt, uint32_t grid,
                               uint32_t lds_bytes, hipStream_t stream);
 hipError_t copk_stream_occupancy(int fw_mode, int lpm_mode, int ppt, uint32_t lds_bytes, int *blocks_per_cu);
-// persistent globally ordered kernel (cop_sweep.hip): tiles claimed from
-// p->tickets[0] in chunks; any grid size (no residency assumption);
-// 320-thread workgroups (4 data waves + 1 coordinator)
-hipError_t copk_launch_sweep(const CopKParams *p, int fw_mode, int lpm_mode, int ppt, uint32_t grid,
-                             uint32_t lds_bytes, hipStream_t stream);
-hipError_t copk_sweep_occupancy(int fw_mode, int lpm_mode, int ppt, uint32_t lds_bytes, int *blocks_per_cu);
 // dst[i] = src[i] (atomic load) or atomic exchange with 0 when reset
 hipError_t copk_snapshot(unsigned long long *src, uint32_t n_words, unsigned long long *dst, int reset,
                          hipStream_t stream);

@@ -156,8 +156,6 @@ struct cop_ctx {
     int kernel_mode = COP_KERNEL_AUTO;   // cop_set_kernel_mode / $COP_KERNEL
     int stream_ppt = 4;        // streaming kernel tile = 256 * stream_ppt ($COP_STREAM_PPT 1, 2, 4)
     int stream_occ = 2;        // streaming kernel workgroups per CU, at most ($COP_STREAM_OCC)
-    int sweep_ppt = 4;         // sweep kernel tile = 256 * sweep_ppt ($COP_SWEEP_PPT 1, 2, 4)
-    int sweep_occ = 2;         // sweep kernel workgroups per CU, at most ($COP_SWEEP_OCC)
     uint32_t stream_min_batches = 0xFFFFFFFFu;   // auto: batch-sweep kernel from this many batches (off; $COP_STREAM_MIN_BATCHES)
     int occ_key = -1, occ_val = 0;   // cached occupancy query
     bool coalesced = true;     // one-shot kernel: coalesced header loads where eligible ($COP_LOADS=strided: off)
@@ -403,7 +401,6 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_KERNEL")) {
         if (!strcmp(e, "oneshot")) c->kernel_mode = COP_KERNEL_ONESHOT;
         else if (!strcmp(e, "stream")) c->kernel_mode = COP_KERNEL_STREAM;
-        else if (!strcmp(e, "sweep")) c->kernel_mode = COP_KERNEL_SWEEP;
     }
     if (const char *e = getenv("COP_LOADS")) c->coalesced = strcmp(e, "strided") != 0;
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
@@ -415,14 +412,6 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_STREAM_OCC")) {
         int v = atoi(e);
         if (v >= 1 && v <= 8) c->stream_occ = v;
-    }
-    if (const char *e = getenv("COP_SWEEP_PPT")) {
-        int v = atoi(e);
-        if (v == 1 || v == 2 || v == 4) c->sweep_ppt = v;
-    }
-    if (const char *e = getenv("COP_SWEEP_OCC")) {
-        int v = atoi(e);
-        if (v >= 1 && v <= 8) c->sweep_occ = v;
     }
     if (const char *e = getenv("COP_STREAMS")) {
         int v = atoi(e);
@@ -643,24 +632,16 @@ static int choose_ppt(const cop_ctx *c, uint64_t total)
 // Which kernel runs a launch, and its tile size (256 * ppt packets).
 struct Plan {
     bool stream;
-    bool sweep;
     int ppt;
     int layout;   // one-shot kernel: COPK_LAY_*
 };
 
-static Plan plan_launch(const cop_ctx *c, uint64_t total, uint32_t nb, bool imix, uint32_t min_stride, bool demux)
+static Plan plan_launch(const cop_ctx *c, uint64_t total, uint32_t nb, bool imix, uint32_t min_stride)
 {
     const bool eligible = !imix && min_stride >= COPK_STREAM_MIN_STRIDE;
-    Plan pl{false, false, choose_ppt(c, total),
+    Plan pl{false, choose_ppt(c, total),
             imix ? COPK_LAY_IMIX : (eligible && c->coalesced) ? COPK_LAY_COALESCED : COPK_LAY_SLOTS};
     if (!eligible || c->kernel_mode == COP_KERNEL_ONESHOT) return pl;
-    if (c->kernel_mode == COP_KERNEL_SWEEP) {
-        if (!demux) {
-            pl.sweep = true;
-            pl.ppt = c->sweep_ppt;
-        }
-        return pl;
-    }
     // the batch-sweep kernel runs one workgroup per batch: worth it when
     // there are batches for every CU and each is many tiles long
     const uint64_t per_batch = nb ? total / nb : 0;
@@ -684,7 +665,6 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     HIPCHK(c, hipSetDevice(c->device));
     // one chain per port (demux); the batch-sweep kernel needs none
     const uint32_t look_need = pl.stream ? 0u : p.ntiles * (p.demux ? p.demux : 1u);
-    if (pl.sweep && p.demux) return set_err(c, -EINVAL, "sweep kernel: no per-port demux");
     if (look_need > L.look_cap) {
         // grow this lane's look-back words (stream order: free after its work)
         HIPCHK(c, hipStreamSynchronize(L.s));
@@ -725,13 +705,9 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     off += 2 * p.lpm_m;
     p.lds_misc_off = off;
     if (pl.stream) off += COPK_LDS_STREAM_MISC_WORDS;
-    else if (pl.sweep) off += COPK_LDS_SWEEP_MISC_WORDS;
     else off += (p.demux || (c->cfg.flags & COP_CFG_PORT_STATS)) ? COPK_LDS_MISC_EXT_WORDS : COPK_LDS_MISC_WORDS;
     p.lds_stage_off = 0;
-    if (pl.sweep && p.compact && c->stage_lists) {
-        p.lds_stage_off = off;   // two tiles' forward lists (by tile parity)
-        off += 2 * COPK_BLOCK * ppt;
-    } else if (!pl.stream && !pl.sweep && p.compact && !p.demux && c->stage_lists) {
+    if (!pl.stream && p.compact && !p.demux && c->stage_lists) {
         p.lds_stage_off = off;   // the tile's forward list, written out in 16-byte stores
         off += COPK_BLOCK * ppt;
     }
@@ -751,36 +727,31 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     p.stamps = c->stamps;
     if ((c->dbg & 8u) && p.ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
     uint32_t grid = p.ntiles;   // one-shot: one tile per workgroup
-    if (pl.stream || pl.sweep) {
+    if (pl.stream) {
         // persistent: no more workgroups than are co-resident, at most
-        // stream_occ / sweep_occ per CU
-        const int key = (((fw_mode * 4 + lpm_mode) * 8 + ppt) * (160 * 1024 + 1) + (int)lds_bytes) * 2 + (pl.sweep ? 1 : 0);
+        // stream_occ per CU
+        const int key = ((fw_mode * 4 + lpm_mode) * 8 + ppt) * (160 * 1024 + 1) + (int)lds_bytes;
         if (key != c->occ_key) {
             int occ = 0;
-            hipError_t oe = pl.sweep ? copk_sweep_occupancy(fw_mode, lpm_mode, ppt, lds_bytes, &occ)
-                                     : copk_stream_occupancy(fw_mode, lpm_mode, ppt, lds_bytes, &occ);
+            hipError_t oe = copk_stream_occupancy(fw_mode, lpm_mode, ppt, lds_bytes, &occ);
             if (oe != hipSuccess || occ < 1)
-                return set_err(c, -EIO, "persistent kernel occupancy: %s (%d)", hipGetErrorString(oe), occ);
+                return set_err(c, -EIO, "stream kernel occupancy: %s (%d)", hipGetErrorString(oe), occ);
             c->occ_key = key;
             c->occ_val = occ;
         }
-        const uint64_t resident =
-            (uint64_t)c->ncu * (uint64_t)std::min(c->occ_val, pl.sweep ? c->sweep_occ : c->stream_occ);
-        // stream: one workgroup per batch at a time; sweep: one per tile at most
-        grid = (uint32_t)std::min<uint64_t>(pl.sweep ? p.ntiles : p.nb, resident);
+        const uint64_t resident = (uint64_t)c->ncu * (uint64_t)std::min(c->occ_val, c->stream_occ);
+        grid = (uint32_t)std::min<uint64_t>(p.nb, resident);   // one workgroup per batch at a time
     }
 
     if (c->timing) {
         if (L.ev_count == TIMING_SLOTS) harvest_one(c, L);
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][0], L.s));
     }
-    hipError_t e = pl.stream  ? copk_launch_stream(&p, fw_mode, lpm_mode, ppt, grid, lds_bytes, L.s)
-                   : pl.sweep ? copk_launch_sweep(&p, fw_mode, lpm_mode, ppt, grid, lds_bytes, L.s)
-                              : copk_launch(&p, fw_mode, lpm_mode, pl.layout, ppt, grid, lds_bytes, L.s);
+    hipError_t e = pl.stream ? copk_launch_stream(&p, fw_mode, lpm_mode, ppt, grid, lds_bytes, L.s)
+                             : copk_launch(&p, fw_mode, lpm_mode, pl.layout, ppt, grid, lds_bytes, L.s);
     if (e != hipSuccess) return set_err(c, -EIO, "launch: %s", hipGetErrorString(e));
     L.dirty[q ^ 1] = 0;
-    // ticket lines this launch dirtied: one per batch (one-shot), line 0 (sweep)
-    L.dirty[q] = pl.sweep ? 1u : (p.compact && !(c->dbg & 2u) && !pl.stream) ? nb_used : 0;
+    L.dirty[q] = (p.compact && !(c->dbg & 2u) && !pl.stream) ? nb_used : 0;
     L.parity = q ^ 1;
     if (c->timing) {
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][1], L.s));
@@ -817,8 +788,7 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb,
     uint32_t min_stride = 0xFFFFFFFFu;
     for (uint32_t i = 0; i < nb; i++)
         if (batches[i].n) min_stride = std::min(min_stride, batches[i].stride);
-    const Plan pl = plan_launch(c, total, nb, imix, min_stride,
-                                demux && compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS));
+    const Plan pl = plan_launch(c, total, nb, imix, min_stride);
     const uint32_t tile = COPK_BLOCK * pl.ppt;
     uint32_t ntiles = 0;
     for (uint32_t i = 0; i < nb; i++) {
@@ -864,8 +834,7 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     const uint32_t lists = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 1u;
     if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < (uint64_t)r->n * lists))
         return set_err(c, -EINVAL, "ring: slot sizes smaller than n (x ports with demux)");
-    const Plan pl = plan_launch(c, (uint64_t)r->n * count, count, imix, r->stride,
-                                compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS));
+    const Plan pl = plan_launch(c, (uint64_t)r->n * count, count, imix, r->stride);
     const uint32_t tile = COPK_BLOCK * pl.ppt;
     const uint32_t tpb = r->n ? (r->n + tile - 1) / tile : 1;
     CopKParams p;
@@ -897,7 +866,7 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
 
 int cop_set_kernel_mode(cop_ctx *c, int mode)
 {
-    if (!c || mode < COP_KERNEL_AUTO || mode > COP_KERNEL_SWEEP) return -EINVAL;
+    if (!c || mode < COP_KERNEL_AUTO || mode > COP_KERNEL_STREAM) return -EINVAL;
     c->kernel_mode = mode;
     return 0;
 }

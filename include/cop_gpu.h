@@ -302,15 +302,11 @@ int  cop_set_host_threads(cop_ctx *ctx, uint32_t n);
  * COP_KERNEL_AUTO (default) runs one workgroup per tile (the faster form at
  * every measured shape); STREAM uses the persistent batch-sweep kernel (one
  * workgroup sweeps a whole batch) whenever the launch is eligible (packet
- * batches at stride >= 48, no IMIX offsets); SWEEP uses the persistent
- * globally ordered kernel (a few workgroups per CU claim tiles in order and
- * prefetch the next one; same eligibility, and no per-port demux); ONESHOT
- * never uses either.
- * Also $COP_KERNEL = auto | oneshot | stream | sweep. */
+ * batches at stride >= 48, no IMIX offsets); ONESHOT never.
+ * Also $COP_KERNEL = auto | oneshot | stream. */
 #define COP_KERNEL_AUTO    0
 #define COP_KERNEL_ONESHOT 1
 #define COP_KERNEL_STREAM  2
-#define COP_KERNEL_SWEEP   3
 int  cop_set_kernel_mode(cop_ctx *ctx, int mode);
 
 /* Counters (u64, device-resident, summed over every submitted packet).

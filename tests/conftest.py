@@ -30,24 +30,13 @@ def _ensure_built():
 _ensure_built()
 
 
-@pytest.fixture(params=["auto", "stream", "sweep"])
+@pytest.fixture(params=["auto", "stream"])
 def kernel_mode(request):
-    """Every GPU test runs three times: with the library's own kernel choice
-    (small launches take the one-tile-per-workgroup kernel), and with each
-    persistent kernel forced wherever the launch is eligible (the batch-sweep
-    kernel, and the globally ordered sweep kernel). All must give the same
-    bit-exact results."""
+    """Every GPU test runs twice: with the library's own kernel choice (small
+    launches take the one-tile-per-workgroup kernel) and with the persistent
+    streaming kernel forced wherever the launch is eligible. Both must give
+    the same bit-exact results."""
     return request.param
-
-
-@pytest.fixture
-def persistent_mode(kernel_mode):
-    """The persistent kernel a test that forces one should use under this
-    parametrisation: the sweep kernel under "sweep", else the batch-sweep
-    (stream) kernel."""
-    import copgpu as cg
-
-    return cg.KERNEL_SWEEP if kernel_mode == "sweep" else cg.KERNEL_STREAM
 
 
 @pytest.fixture
@@ -57,7 +46,7 @@ def gpu_ctx_factory(kernel_mode):
     if cg.device_count() < 1:
         pytest.fail("GPU test on a machine without a visible GPU")
     made = []
-    mode = {"auto": cg.KERNEL_AUTO, "stream": cg.KERNEL_STREAM, "sweep": cg.KERNEL_SWEEP}[kernel_mode]
+    mode = {"auto": cg.KERNEL_AUTO, "stream": cg.KERNEL_STREAM}[kernel_mode]
 
     def make(**kw):
         c = cg.Context(**kw)

@@ -1,10 +1,9 @@
-"""GPU parity at bench-scale launch shapes for the three kernels: the one-shot
+"""GPU parity at bench-scale launch shapes for both kernels: the one-shot
 kernel (csrc/cop_kernels.hip: coalesced loads, batches interleaved over
-workgroups, LDS-staged forward lists), the persistent batch-sweep kernel
-(csrc/cop_stream.hip) and the persistent globally ordered sweep kernel
-(csrc/cop_sweep.hip), plus the hand-offs between them on one launch lane.
+workgroups, LDS-staged forward lists) and the persistent batch-sweep kernel
+(csrc/cop_stream.hip), plus the hand-offs between the two on one launch lane.
 
-Every other GPU test also runs with each persistent kernel forced
+Every other GPU test also runs with the batch-sweep kernel forced
 (conftest.kernel_mode), so these add the large-launch shapes: batch rings of
 64k-packet slots (the bench's layout), DIR-24-8 stages, demux and port
 statistics, rule counters, and non-uniform descriptor batches. Bit-exact
@@ -117,11 +116,11 @@ def test_stream_fw_lpm_dir24(gpu_ctx_factory, fw_dir):
     check_slots(res, fwd, cnt, ro, fos, B, range(P))
 
 
-def test_stream_mbuf_layout_ring(gpu_ctx_factory, persistent_mode):
+def test_stream_mbuf_layout_ring(gpu_ctx_factory):
     """Slots at mbuf stride (2176 B) with 128 B headroom, streaming kernel."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F)
-    ctx.set_kernel_mode(persistent_mode)
+    ctx.set_kernel_mode(cg.KERNEL_STREAM)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     B, P = 30000 + 5, 5
     pk = cg.gen_trace(0x5EED0A20, B * P, rules)
@@ -131,12 +130,12 @@ def test_stream_mbuf_layout_ring(gpu_ctx_factory, persistent_mode):
     check_slots(res, fwd, cnt, ro, fos, B, range(P))
 
 
-def test_stream_descriptor_ragged_batches(gpu_ctx_factory, persistent_mode):
+def test_stream_descriptor_ragged_batches(gpu_ctx_factory):
     """Descriptor submit with non-uniform batches (0, 1, 255, 1025, 70000,
     and large ones): the tile -> batch scan of the streaming kernel."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F)
-    ctx.set_kernel_mode(persistent_mode)
+    ctx.set_kernel_mode(cg.KERNEL_STREAM)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     sizes = [0, 1, 255, 1025, 70000, 262144, 3, 200000, 0, 131072]
     n = sum(sizes)
@@ -211,9 +210,8 @@ def test_kernel_handoffs_on_one_lane(gpu_ctx_factory):
     df = ctx.alloc(B * P * 4)
     dc = ctx.alloc(P * 4)
     ring = cg.make_ring(dp, P, B, dr, slot_bytes, stride=64, fwd_idx=df, fwd_slot=B, fwd_count=dc)
-    modes = [cg.KERNEL_ONESHOT, cg.KERNEL_STREAM, cg.KERNEL_SWEEP, cg.KERNEL_STREAM, cg.KERNEL_ONESHOT,
-             cg.KERNEL_SWEEP, cg.KERNEL_SWEEP, cg.KERNEL_ONESHOT, cg.KERNEL_ONESHOT, cg.KERNEL_STREAM,
-             cg.KERNEL_ONESHOT]
+    modes = [cg.KERNEL_ONESHOT, cg.KERNEL_STREAM, cg.KERNEL_STREAM, cg.KERNEL_ONESHOT, cg.KERNEL_ONESHOT,
+             cg.KERNEL_STREAM, cg.KERNEL_ONESHOT]
     for i, m in enumerate(modes * 3):
         ctx.set_kernel_mode(m)
         ctx.submit_ring(ring, i % P, P)
@@ -228,12 +226,12 @@ def test_kernel_handoffs_on_one_lane(gpu_ctx_factory):
     assert c["rx"] == B * P * len(modes) * 3
 
 
-def test_stream_rule_counters(gpu_ctx_factory, persistent_mode):
+def test_stream_rule_counters(gpu_ctx_factory):
     """Per-rule hit counters under the streaming kernel equal the oracle's
     per-rule hits summed over the launch."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_RULE_COUNTERS)
-    ctx.set_kernel_mode(persistent_mode)
+    ctx.set_kernel_mode(cg.KERNEL_STREAM)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     B, P = 65536, 8
     pk = cg.gen_trace(0x5EED0A60, B * P, rules)
