@@ -45,11 +45,14 @@ __device__ __forceinline__ unsigned long long lb_load(unsigned long long *p)
 // granules, counters) is ordered by agent-scope atomics, not by barriers.
 // LDS-DMA (global_load_lds) completion is counted by vmcnt: wait for staged
 // tables with __syncthreads().
+// (A fence restricted to LDS, __builtin_amdgcn_fence(..., "workgroup",
+// "local"), does this in small kernels but loses its address-space tag in
+// the pipeline kernels and falls back to vmcnt(0).) The memory clobber
+// keeps the compiler from moving memory accesses across the barrier;
+// lgkmcnt(0) completes this wave's LDS writes before it arrives.
 __device__ __forceinline__ void lds_barrier()
 {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 __device__ __forceinline__ void lds_stage(uint32_t *lds_dst, const void *gsrc, uint32_t n16, int lane, int wave)
