@@ -116,15 +116,19 @@ __global__ __launch_bounds__(BLOCK, 2) void cop_stream(const CopKParams p)
         }
     };
     skip_empty(b, B);
-    Slots<PPT> cur;
-    if (b < p.nb) load(B, 0, cur);
+    // ping-pong tile buffers: the loop runs two tiles per trip, so the tile
+    // in flight never has to be copied into the tile in hand (a copy waits
+    // for the loads to land and ends the overlap)
+    Slots<PPT> bufA, bufB;
+    if (b < p.nb) load(B, 0, bufA);
     __syncthreads();   // LDS tables landed (the barrier waits for the DMA)
 
     Counts cn;
     uint32_t prx[COPK_MAX_DEMUX_PORTS] = {}, ptx[COPK_MAX_DEMUX_PORTS] = {};
     uint32_t run[COPK_MAX_DEMUX_PORTS] = {};   // forward-list lengths so far (wave-uniform)
     uint32_t par = 0;
-    while (b < p.nb) {
+    // one tile: classify `cur` while `nxt` loads; false after the last tile
+    auto step = [&](Slots<PPT> &cur, Slots<PPT> &nxt) -> bool {
         // ---- the next tile: this batch's, or the first of the next batch ----
         uint32_t bn = b, tn = t + 1;
         CopKBatch Bn = B;
@@ -137,8 +141,11 @@ __global__ __launch_bounds__(BLOCK, 2) void cop_stream(const CopKParams p)
             }
         }
         const bool more = bn < p.nb;
-        Slots<PPT> nxt;
         if (EARLY && more) load(Bn, tn, nxt);
+        // keep the prefetch ahead of this tile's gathers: without the fence
+        // the scheduler sinks the loads below the ds_bpermutes, which wait
+        // for this tile's data, and nothing is in flight while it is used
+        __builtin_amdgcn_sched_barrier(0);
 
         // ---- fields to the packet's lane ----
         uint32_t w3[PPT], w6[PPT], w7[PPT], w8[PPT];
@@ -153,6 +160,7 @@ __global__ __launch_bounds__(BLOCK, 2) void cop_stream(const CopKParams p)
         pass1<FW, LPM, PPT>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe);
         pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, cn.total, cn.notv4);
         if (!EARLY && more) load(Bn, tn, nxt);
+        __builtin_amdgcn_sched_barrier(0);
         rule_hit_atomics<FW, PPT>(p, valid, flags, fwe);
         bool fwd[PPT];
         store_records<PPT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn);
@@ -208,11 +216,15 @@ __global__ __launch_bounds__(BLOCK, 2) void cop_stream(const CopKParams p)
 #pragma unroll
             for (int q = 0; q < COPK_MAX_DEMUX_PORTS; q++) run[q] = 0;
         }
-        if (!more) break;
+        if (!more) return false;
         b = bn;
         t = tn;
         B = Bn;
-        cur = nxt;
+        return true;
+    };
+    if (b < p.nb) {
+        while (step(bufA, bufB) && step(bufB, bufA)) {
+        }
     }
     flush_counters(p, cn, prx, ptx, misc + SM_RED, misc + SM_PS, tid, lane, wave);
 }
