@@ -15,6 +15,8 @@ brackets the timed region and the max elapsed time over ranks is used.
 Also reported (rank 0):
   roofline      algorithmic bytes per launch / mean kernel time (HIP events
                 on the context's stream around every launch), vs 8 TB/s;
+                box_ceiling: what the same box sustains for the same byte mix
+                with no classification (tools/ceiling.hip), same pool;
   cpu_baseline  the oracle's restatement of the reference CPU coprocessor()
                 loop (oracle/cop_oracle.c), 1 pinned core, bounded sample.
 """
@@ -53,6 +55,29 @@ WORKLOADS = {
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def box_ceiling(pkts_addr, n_slots, out_addr):
+    """GB/s of the 72 B/packet copy mix on this box (None if the tool is absent)."""
+    import ctypes
+
+    path = os.path.join(ROOT, "tools", "libceiling.so")
+    if not os.path.exists(path):
+        log("[bench] tools/libceiling.so not built: no box ceiling")
+        return None
+    lib = ctypes.CDLL(path)
+    fn = lib.ceiling_copy_mix
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                   ctypes.POINTER(ctypes.c_float)]
+    fn.restype = ctypes.c_int
+    best = None
+    for m in (4, 8, 16):
+        ms = ctypes.c_float(0.0)
+        if fn(pkts_addr, n_slots, out_addr, m, 5, ctypes.byref(ms)) == 0 and ms.value > 0:
+            best = ms.value if best is None else min(best, ms.value)
+    if best is None:
+        return None
+    return 72.0 * n_slots / (best * 1e-3) / 1e9
 
 
 def main():
@@ -197,6 +222,12 @@ def main():
     alg_bytes = bytes_per_pkt * B * Lb
     achieved = alg_bytes / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
 
+    # the same box's streaming ceiling for this byte mix (tools/ceiling.hip):
+    # read every 64 B slot of the pool, write an 8 B record, nothing else
+    ceiling = None
+    if not W["imix"]:
+        ceiling = box_ceiling(d_pkts.addr, P * B, d_res.addr)
+
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_L{Lb}_s{args.streams}.json")
     if os.path.exists(tpath):
@@ -243,6 +274,12 @@ def main():
             "traffic_per_algorithmic": (round(traffic / alg_bytes, 4) if traffic else None),
             "kernel_ms_per_launch": round(mean_ms, 6),
             "launches_timed": int(n_launch),
+            "box_ceiling": (None if ceiling is None else {
+                "what": "same pool, same process: read each 64 B slot + write an 8 B record, no classification "
+                        "(tools/ceiling.hip, best of grids 4/8/16 x CUs)",
+                "achieved": round(ceiling, 2), "unit": "GB/s",
+                "frac_of_peak": round(ceiling / HBM_PEAK_GBS, 4),
+                "pipeline_frac_of_ceiling": round(achieved / ceiling, 4)}),
         },
         "cpu_baseline": None,
     }
