@@ -214,6 +214,21 @@ def main():
     mean_ms, n_launch = ctx.launch_timing_read(reset=True)
     ctx.launch_timing(False)
     cnt = ctx.counters()
+
+    # ---- single-batch latency: one batch per launch, nothing
+    # else in flight; kernel time from HIP events, submit->sync on the host ----
+    n_lat = 50
+    host_us = []
+    ctx.launch_timing(True)
+    for i in range(n_lat):
+        h0 = time.perf_counter()
+        ctx.submit_ring(ring, i % P, 1)
+        ctx.sync()
+        host_us.append((time.perf_counter() - h0) * 1e6)
+    lat_ms, _ = ctx.launch_timing_read(reset=True)
+    ctx.launch_timing(False)
+    single_batch = {"batch": B, "launches": n_lat, "kernel_us_mean": round(lat_ms * 1e3, 2),
+                    "host_submit_to_sync_us_median": round(float(np.median(host_us)), 2)}
     fwd_frac = cnt["forward"] / max(1, cnt["rx"])
     # algorithmic bytes per packet: the 64 B header line (+4 B offset for
     # IMIX), the 8 B result record, and 4 B per forwarded packet for the
@@ -283,6 +298,7 @@ def main():
         },
         "cpu_baseline": None,
     }
+    out["single_batch_latency"] = single_batch
     if reduce_info:
         out["counter_reduce"] = reduce_info
 
