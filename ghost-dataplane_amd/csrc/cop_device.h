@@ -301,6 +301,22 @@ __device__ __forceinline__ void gather_step(const StepGeom &g, const u32x4 (&v)[
     w8 = (uint32_t)__builtin_amdgcn_ds_bpermute(g.a8, (int)c2x);
 }
 
+// The launch's optional features. A kernel instantiated without them
+// (cop_kernels.hip EXT == false) passes all-zero options, so the compiler
+// drops their code: the hot configuration's kernel is about half the size,
+// and every launch starts with cold instruction caches.
+struct Opt {
+    uint32_t demux;                  // one ordered forward list per port
+    uint32_t port_stats;             // per-port counters for ports < port_stats
+    uint32_t dbg;                    // timing-only ablations ($COP_DBG)
+    unsigned long long *rule_hits;   // per-rule FW hit counters or nullptr
+};
+
+__device__ __forceinline__ Opt opt_all(const CopKParams &p)
+{
+    return Opt{p.demux, p.port_stats, p.dbg, p.rule_hits};
+}
+
 // LDS views of the tables (staged at workgroup start)
 struct Tables {
     const uint32_t *rt_top;
@@ -402,14 +418,14 @@ __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[
 // Per-rule hit counters: one relaxed device-scope u64 add per FW-stage hit
 // (no return value: fire-and-forget atomics at the L2/fabric).
 template <int FW, int PPT>
-__device__ __forceinline__ void rule_hit_atomics(const CopKParams &p, const bool (&valid)[PPT],
+__device__ __forceinline__ void rule_hit_atomics(const Opt &o, const bool (&valid)[PPT],
                                                  const uint32_t (&flags)[PPT], const uint32_t (&fwe)[PPT])
 {
-    if (FW != COPK_TBL_OFF && p.rule_hits) {
+    if (FW != COPK_TBL_OFF && o.rule_hits) {
 #pragma unroll
         for (int k = 0; k < PPT; k++)
             if (valid[k] && (flags[k] & COPK_FLAG_FW_HIT))
-                __hip_atomic_fetch_add(&p.rule_hits[fwe[k] & 0x00FFFFFFu], 1ull, __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(&o.rule_hits[fwe[k] & 0x00FFFFFFu], 1ull, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -495,12 +511,13 @@ struct CompactLds {
 // record stores go there, so the look-back's loads (vmcnt retires in order)
 // do not wait for them and the other waves store while wave 0 looks back.
 template <int PPT, typename Mid>
-__device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatch &B, uint32_t lb_off, uint32_t j,
+__device__ __forceinline__ void compact_tile(const CopKParams &p, const Opt &o, const CopKBatch &B, uint32_t lb_off,
+                                             uint32_t j,
                                              uint32_t base, const bool (&fwd)[PPT], const uint32_t (&port)[PPT],
                                              const CompactLds &s, int tid, int lane, int wave, Mid mid)
 {
     constexpr int NQ = PPT * WAVES;
-    if (!p.demux) {
+    if (!o.demux) {
         unsigned long long bal[PPT];
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
@@ -514,7 +531,7 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatc
         uint32_t off[PPT];
 #pragma unroll
         for (int k = 0; k < PPT; k++) off[k] = (uint32_t)__shfl((int)ex, k * WAVES + wave);
-        const bool staged = s.stage != nullptr && B.fwd_idx && !(p.dbg & 64u);
+        const bool staged = s.stage != nullptr && B.fwd_idx && !(o.dbg & 64u);
         if (staged) {
             // the tile's list in LDS, in order, while wave 0 looks back
 #pragma unroll
@@ -527,7 +544,7 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatc
         if (wave == 0) {
             // dbg bit 32 (timing-only ablation): no look-back wait, wrong offsets
             const uint32_t excl =
-                (p.dbg & 32u) ? j * 1024u : look_back(p.look + lb_off, 1u, j, agg, p.epoch, p.err, lane);
+                (o.dbg & 32u) ? j * 1024u : look_back(p.look + lb_off, 1u, j, agg, p.epoch, p.err, lane);
             if (lane == 0) {
                 *s.pref = excl;
                 if (B.fwd_count && j == B.ntiles - 1) *B.fwd_count = excl + agg;
@@ -538,7 +555,7 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatc
         const uint32_t pref = *s.pref;
         if (staged) {
             copy_out_list(B.fwd_idx, pref, agg, s.stage, tid);
-        } else if (B.fwd_idx && !(p.dbg & 64u)) {
+        } else if (B.fwd_idx && !(o.dbg & 64u)) {
 #pragma unroll
             for (int k = 0; k < PPT; k++) {
                 if (fwd[k]) {
@@ -550,7 +567,7 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const CopKBatc
         }
         return;
     }
-    const uint32_t K = p.demux;
+    const uint32_t K = o.demux;
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         for (uint32_t q = 0; q < K; q++) {
@@ -613,7 +630,7 @@ __device__ __forceinline__ void port_counts(uint32_t K, const bool (&valid)[PPT]
 // workgroup, into one of COPK_COUNTER_SHARDS shards (a 128-byte line each)
 // so no single word serialises thousands of atomics; then the per-port
 // counters the same way. s_red: WAVES*8 words, s_ps: WAVES*16 words.
-__device__ __forceinline__ void flush_counters(const CopKParams &p, const Counts &cn,
+__device__ __forceinline__ void flush_counters(const CopKParams &p, const Opt &o, const Counts &cn,
                                                const uint32_t (&prx)[COPK_MAX_DEMUX_PORTS],
                                                const uint32_t (&ptx)[COPK_MAX_DEMUX_PORTS], uint32_t *s_red,
                                                uint32_t *s_ps, int tid, int lane, int wave)
@@ -630,7 +647,7 @@ __device__ __forceinline__ void flush_counters(const CopKParams &p, const Counts
 #pragma unroll
         for (int q = 0; q < 8; q++) s_red[wave * 8 + q] = c[q];
     }
-    const uint32_t K = p.port_stats;
+    const uint32_t K = o.port_stats;
     if (K && lane == 0 && wave < WAVES) {
 #pragma unroll
         for (int q = 0; q < COPK_MAX_DEMUX_PORTS; q++) {
@@ -662,7 +679,7 @@ __device__ __forceinline__ void flush_counters(const CopKParams &p, const Counts
         case 7: v = r[6]; break;
         default: v = r[7]; break;
         }
-        if (v && !(p.dbg & 1u))
+        if (v && !(o.dbg & 1u))
             atomicAdd(&p.counters[(blockIdx.x % COPK_COUNTER_SHARDS) * 16 + tid], (unsigned long long)v);
     }
     if (K && tid < 2 * K) {

@@ -42,7 +42,7 @@ using namespace copd;
 // s_memrealtime (100 MHz) per phase into a buffer nothing else reads
 #define STAMP(ph)                                                                          \
     do {                                                                                   \
-        if ((p.dbg & 8u) && tid == 0) {                                                    \
+        if ((o.dbg & 8u) && tid == 0) {                                                    \
             __builtin_amdgcn_sched_barrier(0);                                             \
             p.stamps[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime();            \
             __builtin_amdgcn_sched_barrier(0);                                             \
@@ -57,10 +57,13 @@ using namespace copd;
 // (slab + offsets), COPK_LAY_COALESCED (strides >= 48: a wave's 64
 // consecutive packets by three 16-byte non-temporal loads per lane,
 // cop_device.h load_step / gather_step)
-template <int FW, int LPM, int LAY, int PPT>
+// EXT: the launch uses an optional feature (demux, port stats, per-rule
+// counters, $COP_DBG ablations); without, their code is compiled out.
+template <int FW, int LPM, int LAY, int PPT, bool EXT>
 __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const CopKParams p)
 {
     constexpr bool IMIX = LAY == COPK_LAY_IMIX;
+    const Opt o = EXT ? opt_all(p) : Opt{0u, 0u, 0u, nullptr};
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     constexpr int TILE = BLOCK * PPT;
     const int tid = threadIdx.x;
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
     // tile's predecessors have normally published their counts by the time
     // its look-back reads them. Unequal batches: blockIdx ranges.
     const uint32_t g = blockIdx.x;
-    const bool ilv = p.uniform_ntiles != 0 && !(p.dbg & 256u);
+    const bool ilv = p.uniform_ntiles != 0 && !(o.dbg & 256u);
     const uint32_t b = ilv ? __builtin_amdgcn_readfirstlane(g % p.nb) : batch_of_tile(p, g);
     uint32_t look_off;
     const CopKBatch B = batch_desc(p, b, &look_off);
@@ -111,12 +114,12 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
 
     // ---- tile index inside the batch: this batch's ticket counter (or the
     // static order when no look-back runs: p.compact == 0) ----
-    const bool dyn = p.compact != 0 && !(p.dbg & 2u);
+    const bool dyn = p.compact != 0 && !(o.dbg & 2u);
     unsigned long long tk = 0;
     if (dyn && tid == 0) tk = atomicAdd(&p.tickets[b * 16], 1ull);
 
     // ---- stage tables into LDS by LDS-DMA while the ticket is in flight ----
-    if (!(p.dbg & 4u)) {
+    if (!(o.dbg & 4u)) {
         lds_stage(rt_top, p.rt_top, 64, lane, wave);
         lds_stage((uint32_t *)rt_leaf, p.rt_leaf, p.rt_nleaf * 32u, lane, wave);
         if (FW == COPK_TBL_IVT) {
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
     // ---- pass 1 (parse, route, LDS searches, tbl24 loads issued) ----
     uint32_t verdict[PPT], port[PPT], flags[PPT], rnh[PPT], fwe[PPT], lpe[PPT], src[PPT], dst[PPT];
     pass1<FW, LPM, PPT>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe);
-    if (p.dbg & 8u) {
+    if (o.dbg & 8u) {
         uint32_t x = 0;
 #pragma unroll
         for (int k = 0; k < PPT; k++) x ^= verdict[k] ^ src[k];
@@ -187,8 +190,8 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
     // ---- pass 2 (tbl8 step) and the verdicts ----
     Counts cn;
     pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, cn.total, cn.notv4);
-    rule_hit_atomics<FW, PPT>(p, valid, flags, fwe);
-    if (p.dbg & 8u) {
+    rule_hit_atomics<FW, PPT>(o, valid, flags, fwe);
+    if (o.dbg & 8u) {
         uint32_t x = 0;
 #pragma unroll
         for (int k = 0; k < PPT; k++) x ^= verdict[k] ^ rnh[k];
@@ -201,21 +204,23 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
 #pragma unroll
     for (int k = 0; k < PPT; k++) fwd[k] = valid[k] && verdict[k] == COPK_FORWARD;
     auto records = [&] { store_records<PPT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn); };
-    if (p.compact) compact_tile<PPT>(p, B, look_off, j, base, fwd, port, cl, tid, lane, wave, records);
+    if (p.compact) compact_tile<PPT>(p, o, B, look_off, j, base, fwd, port, cl, tid, lane, wave, records);
     else records();
     STAMP(5);
 
     // ---- counters (one flush per workgroup) ----
     uint32_t prx[COPK_MAX_DEMUX_PORTS] = {}, ptx[COPK_MAX_DEMUX_PORTS] = {};
-    if (p.port_stats) port_counts<PPT>(p.port_stats, valid, fwd, port, prx, ptx);
-    flush_counters(p, cn, prx, ptx, s_red, s_ps, tid, lane, wave);
+    if (o.port_stats) port_counts<PPT>(o.port_stats, valid, fwd, port, prx, ptx);
+    flush_counters(p, o, cn, prx, ptx, s_red, s_ps, tid, lane, wave);
     STAMP(6);
 }
 
 template <int FW, int LPM, int LAY, int PPT>
 hipError_t launch_one(const CopKParams &p, uint32_t grid, uint32_t lds_bytes, hipStream_t s)
 {
-    hipLaunchKernelGGL((cop_pipeline<FW, LPM, LAY, PPT>), dim3(grid), dim3(BLOCK), lds_bytes, s, p);
+    const bool ext = p.demux || p.port_stats || p.rule_hits || p.dbg;
+    if (ext) hipLaunchKernelGGL((cop_pipeline<FW, LPM, LAY, PPT, true>), dim3(grid), dim3(BLOCK), lds_bytes, s, p);
+    else hipLaunchKernelGGL((cop_pipeline<FW, LPM, LAY, PPT, false>), dim3(grid), dim3(BLOCK), lds_bytes, s, p);
     return hipGetLastError();
 }
 

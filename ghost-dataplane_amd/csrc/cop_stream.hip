@@ -93,6 +93,7 @@ __global__ __launch_bounds__(BLOCK, 2) void cop_stream(const CopKParams p)
     }
 
     const StepGeom sg = step_geom(lane);
+    const Opt o = opt_all(p);
     const uint32_t K = p.demux ? p.demux : 1u;   // forward lists per batch
     const uint32_t G = gridDim.x;
 
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(BLOCK, 2) void cop_stream(const CopKParams p)
         pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, cn.total, cn.notv4);
         if (!EARLY && more) load(Bn, tn, nxt);
         __builtin_amdgcn_sched_barrier(0);
-        rule_hit_atomics<FW, PPT>(p, valid, flags, fwe);
+        rule_hit_atomics<FW, PPT>(o, valid, flags, fwe);
         bool fwd[PPT];
         store_records<PPT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn);
         if (p.port_stats) port_counts<PPT>(p.port_stats, valid, fwd, port, prx, ptx);
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(BLOCK, 2) void cop_stream(const CopKParams p)
         while (step(bufA, bufB) && step(bufB, bufA)) {
         }
     }
-    flush_counters(p, cn, prx, ptx, misc + SM_RED, misc + SM_PS, tid, lane, wave);
+    flush_counters(p, o, cn, prx, ptx, misc + SM_RED, misc + SM_PS, tid, lane, wave);
 }
 
 template <int FW, int LPM, int PPT>
