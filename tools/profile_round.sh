@@ -14,8 +14,8 @@ mkdir -p "$out"
 export TMPDIR=/tmp
 step() { "$R/tools/gpu_step.sh" "$@" || exit 99; }
 step 400 "$out/stats.log" rocprofv3 --kernel-trace --stats -d "$out/stats" -o bench --output-format csv -- python3 "$R/bench.py" --no-cpu "$@"
-step 400 "$out/pmc_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o bench --output-format csv -- python3 "$R/bench.py" --no-cpu --steps 3840 --warmup 384 "$@"
-step 400 "$out/pmc_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o bench --output-format csv -- python3 "$R/bench.py" --no-cpu --steps 3840 --warmup 384 "$@"
+step 400 "$out/pmc_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o bench --output-format csv -- python3 "$R/bench.py" --no-cpu --steps 3072 --warmup 3072 "$@"
+step 400 "$out/pmc_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o bench --output-format csv -- python3 "$R/bench.py" --no-cpu --steps 3072 --warmup 3072 "$@"
 step 300 "$out/pmc_fetch_mb.log" rocprofv3 --pmc FETCH_SIZE -d "$out/fetch_mb" -o mb --output-format csv -- "$R/tools/membench"
 step 300 "$out/pmc_write_mb.log" rocprofv3 --pmc WRITE_SIZE -d "$out/write_mb" -o mb --output-format csv -- "$R/tools/membench"
 python3 "$R/tools/pmc_traffic.py" "$out/fetch/bench_counter_collection.csv" "$out/write/bench_counter_collection.csv" \
