@@ -26,6 +26,7 @@ static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_LAY_SLOTS 0      /* packet layouts of the one-shot kernel */
 #define COPK_LAY_IMIX 1
 #define COPK_LAY_COALESCED 2
+#define COPK_LAY_HDR16 3      /* packed 16-byte header records (COP_HDR16_STRIDE) */
 
 #define COPK_STAGE_PARSE 0x1u
 

@@ -56,7 +56,8 @@ using namespace copd;
 // LAY: COPK_LAY_SLOTS (per-lane header loads at any stride), COPK_LAY_IMIX
 // (slab + offsets), COPK_LAY_COALESCED (strides >= 48: a wave's 64
 // consecutive packets by three 16-byte non-temporal loads per lane,
-// cop_device.h load_step / gather_step)
+// cop_device.h load_step / gather_step), COPK_LAY_HDR16 (packed 16-byte
+// header records, one 16-byte load per packet: the end-to-end host path)
 // EXT: the launch uses an optional feature (demux, port stats, per-rule
 // counters, $COP_DBG ablations); without, their code is compiled out.
 template <int FW, int LPM, int LAY, int PPT, bool EXT>
@@ -155,6 +156,17 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
         for (int k = 0; k < PPT; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
 #pragma unroll
         for (int k = 0; k < PPT; k++) gather_step(sg, v[k], w3[k], w6[k], w7[k], w8[k]);
+    } else if (LAY == COPK_LAY_HDR16 && B.n) {
+        // one 16-byte record per packet: frame bytes 12..15 then 24..35
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const uint32_t ic = min(base + k * BLOCK + tid, last);
+            const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(B.pkts + B.data_off + (size_t)ic * 16u));
+            w3[k] = v.x;
+            w6[k] = v.y;
+            w7[k] = v.z;
+            w8[k] = v.w;
+        }
     } else if (B.n) {
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
@@ -237,6 +249,7 @@ hipError_t launch_imix(const CopKParams &p, int lay, int ppt, uint32_t grid, uin
 {
     if (lay == COPK_LAY_IMIX) return launch_ppt<FW, LPM, COPK_LAY_IMIX>(p, ppt, grid, lds, s);
     if (lay == COPK_LAY_COALESCED) return launch_ppt<FW, LPM, COPK_LAY_COALESCED>(p, ppt, grid, lds, s);
+    if (lay == COPK_LAY_HDR16) return launch_ppt<FW, LPM, COPK_LAY_HDR16>(p, ppt, grid, lds, s);
     return launch_ppt<FW, LPM, COPK_LAY_SLOTS>(p, ppt, grid, lds, s);
 }
 

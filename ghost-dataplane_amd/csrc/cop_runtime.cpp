@@ -70,8 +70,9 @@ struct Lane {
 };
 
 // Host gather pool for the end-to-end path: the caller and n-1 persistent
-// workers each copy one contiguous slice of the 64-byte header lines into
-// pinned staging (scattered mbuf reads are DRAM-latency bound per thread).
+// workers each pack one contiguous slice of the packets' 16-byte header
+// records into pinned staging (scattered mbuf reads are DRAM-latency bound
+// per thread).
 struct GatherPool {
     std::vector<std::thread> th;
     std::mutex m;
@@ -84,10 +85,16 @@ struct GatherPool {
     uint32_t n = 0;
     int parts = 1;
 
+    // packed header records (COP_HDR16_STRIDE): frame bytes 12..15, 24..35
     static void slice(const void *const *src, uint8_t *dst, uint32_t n, int parts, int i)
     {
         const uint32_t lo = (uint32_t)((uint64_t)n * i / parts), hi = (uint32_t)((uint64_t)n * (i + 1) / parts);
-        for (uint32_t q = lo; q < hi; q++) memcpy(dst + (size_t)q * 64, src[q], 64);
+        for (uint32_t q = lo; q < hi; q++) {
+            const uint8_t *p = (const uint8_t *)src[q];
+            uint8_t *d = dst + (size_t)q * COP_HDR16_STRIDE;
+            memcpy(d, p + 12, 4);
+            memcpy(d + 4, p + 24, 12);
+        }
     }
     void worker(int i)
     {
@@ -639,8 +646,12 @@ struct Plan {
 static Plan plan_launch(const cop_ctx *c, uint64_t total, uint32_t nb, bool imix, uint32_t min_stride)
 {
     const bool eligible = !imix && min_stride >= COPK_STREAM_MIN_STRIDE;
+    const bool hdr16 = !imix && min_stride == COP_HDR16_STRIDE;
     Plan pl{false, choose_ppt(c, total),
-            imix ? COPK_LAY_IMIX : (eligible && c->coalesced) ? COPK_LAY_COALESCED : COPK_LAY_SLOTS};
+            imix    ? COPK_LAY_IMIX
+            : hdr16 ? COPK_LAY_HDR16
+            : (eligible && c->coalesced) ? COPK_LAY_COALESCED
+                                         : COPK_LAY_SLOTS};
     if (!eligible || c->kernel_mode == COP_KERNEL_ONESHOT) return pl;
     // the batch-sweep kernel runs one workgroup per batch: worth it when
     // there are batches for every CU and each is many tiles long
@@ -778,8 +789,10 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb,
         if (b.n > c->cfg.max_batch) return set_err(c, -EINVAL, "batch %u: n %u > max_batch", i, b.n);
         if (b.n && (!b.pkts || !b.results)) return set_err(c, -EINVAL, "batch %u: null pointer", i);
         if (((uintptr_t)b.pkts & 15) || (b.data_off & 15) || (!imix && (b.stride & 15)) ||
-            (!imix && b.stride < 36))
+            (!imix && b.stride < 36 && b.stride != COP_HDR16_STRIDE))
             return set_err(c, -EINVAL, "batch %u: packet starts must be 16-byte aligned", i);
+        if (!imix && b.n && (b.stride == COP_HDR16_STRIDE) != (batches[0].stride == COP_HDR16_STRIDE))
+            return set_err(c, -EINVAL, "batches in one submit must all be header records or all frames");
         if ((uintptr_t)b.results & 7) return set_err(c, -EINVAL, "batch %u: results misaligned", i);
         total += b.n;
         if (b.fwd_idx || b.fwd_count) compact = true;
@@ -828,7 +841,7 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     const bool imix = r->offsets != nullptr;
     if (r->n && (!r->pkts || !r->results)) return set_err(c, -EINVAL, "ring: null pointer");
     if (((uintptr_t)r->pkts & 15) || (r->pkts_slot_bytes & 15) || (r->data_off & 15) ||
-        (!imix && ((r->stride & 15) || r->stride < 36)))
+        (!imix && ((r->stride & 15) || (r->stride < 36 && r->stride != COP_HDR16_STRIDE))))
         return set_err(c, -EINVAL, "ring: packet starts must be 16-byte aligned");
     bool compact = (r->fwd_idx || r->fwd_count) && !(c->cfg.flags & COP_CFG_NO_COMPACT);
     const uint32_t lists = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 1u;
@@ -897,6 +910,11 @@ int cop_poll(cop_ctx *c)
     return 0;
 }
 
+void cop_pack_headers(const void *const *pkt_data, uint32_t n, uint8_t *out)
+{
+    GatherPool::slice(pkt_data, out, n, 1, 0);
+}
+
 static void host_gather(cop_ctx *c, const void *const *src, uint8_t *dst, uint32_t n)
 {
     if (c->gather) c->gather->gather(src, dst, n);
@@ -922,22 +940,22 @@ int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_re
         c->d_fwd = nullptr;
         c->d_fwdn = nullptr;
         c->stage_cap = 0;
-        HIPCHK(c, hipHostMalloc(&c->h_stage, (size_t)cap * 64, hipHostMallocDefault));
-        HIPCHK(c, hipMalloc(&c->d_stage, (size_t)cap * 64));
+        HIPCHK(c, hipHostMalloc(&c->h_stage, (size_t)cap * COP_HDR16_STRIDE, hipHostMallocDefault));
+        HIPCHK(c, hipMalloc(&c->d_stage, (size_t)cap * COP_HDR16_STRIDE));
         HIPCHK(c, hipMalloc(&c->d_res, (size_t)cap * 8));
         HIPCHK(c, hipMalloc(&c->d_fwd, (size_t)cap * 4));
         HIPCHK(c, hipMalloc(&c->d_fwdn, 16));
         c->stage_cap = cap;
     }
     if (int rc0 = sync_lanes(c)) return rc0;   // the staging buffers may still be in use
-    // gather the first 64 bytes of every packet (headers the pipeline reads)
+    // gather the 16 header bytes of every packet the pipeline reads
     host_gather(c, pkt_data, c->h_stage, n);
-    HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, (size_t)n * 64, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_stage, c->h_stage, (size_t)n * COP_HDR16_STRIDE, hipMemcpyHostToDevice, c->stream));
     cop_batch b;
     memset(&b, 0, sizeof(b));
     b.pkts = c->d_stage;
     b.n = n;
-    b.stride = 64;
+    b.stride = COP_HDR16_STRIDE;
     b.results = c->d_res;
     b.fwd_idx = fwd_idx ? c->d_fwd : nullptr;
     b.fwd_count = (fwd_idx || fwd_count) ? c->d_fwdn : nullptr;
@@ -993,9 +1011,9 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
         L.h_stage = L.d_stage = nullptr;
         L.h_res = L.d_res = nullptr;
         L.cap = 0;
-        HIPCHK(c, hipHostMalloc(&L.h_stage, (size_t)batch * 64, hipHostMallocDefault));
+        HIPCHK(c, hipHostMalloc(&L.h_stage, (size_t)batch * COP_HDR16_STRIDE, hipHostMallocDefault));
         HIPCHK(c, hipHostMalloc(&L.h_res, (size_t)batch * 8, hipHostMallocDefault));
-        HIPCHK(c, hipMalloc(&L.d_stage, (size_t)batch * 64));
+        HIPCHK(c, hipMalloc(&L.d_stage, (size_t)batch * COP_HDR16_STRIDE));
         HIPCHK(c, hipMalloc(&L.d_res, (size_t)batch * 8));
         L.cap = batch;
     }
@@ -1005,14 +1023,14 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
         lane = (lane + 1) % c->n_lanes;
         if (int rc = lane_finish(c, L, results)) return rc;
         const uint32_t k = (uint32_t)((n - first) < batch ? (n - first) : batch);
-        // host gather of the 64-byte header lines (overlaps the other lanes)
+        // host gather of the 16-byte header records (overlaps the other lanes)
         host_gather(c, pkt_data + first, L.h_stage, k);
-        HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * 64, hipMemcpyHostToDevice, L.s));
+        HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * COP_HDR16_STRIDE, hipMemcpyHostToDevice, L.s));
         cop_batch b;
         memset(&b, 0, sizeof(b));
         b.pkts = L.d_stage;
         b.n = k;
-        b.stride = 64;
+        b.stride = COP_HDR16_STRIDE;
         b.results = L.d_res;
         if (int rc = submit_on(c, L, &b, 1, false)) return rc;
         HIPCHK(c, hipMemcpyAsync(L.h_res, L.d_res, (size_t)k * 8, hipMemcpyDeviceToHost, L.s));

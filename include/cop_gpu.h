@@ -224,6 +224,16 @@ int  cop_set_routing_table(cop_ctx *ctx, const uint16_t *rt /* 65536 */);
 int  cop_load_fw_rules_file(cop_ctx *ctx, const char *path, const cop_lpm_config *cfg,
                             cop_lpm_report *report);
 
+/* Packed header records: a batch (or ring) with stride == COP_HDR16_STRIDE
+ * and no offsets holds, instead of frames, one 16-byte record per packet:
+ * frame bytes 12..15 (EtherType, version/IHL, TOS) followed by bytes 24..35
+ * (IPv4 checksum, src, dst, UDP ports), the only bytes the pipeline reads.
+ * Results are identical to the frames'. cop_pack_headers() builds them on
+ * the host; the end-to-end host path moves 16 bytes per packet over PCIe
+ * this way instead of a 64-byte header line. */
+#define COP_HDR16_STRIDE 16u
+void cop_pack_headers(const void *const *pkt_data, uint32_t n, uint8_t *out /* n * 16 bytes */);
+
 /* One batch of packets resident in device memory (HBM).
  * Packet i starts at  pkts + (offsets ? offsets[i] : i * stride) + data_off.
  * Every packet start must be 16-byte aligned and hold >= 48 readable bytes

@@ -2,8 +2,9 @@
 """End-to-end rate of the host-memory path (north star: "packets start and
 end in host memory ... pinned hipMemcpyAsync in and out"): packets sit in an
 mbuf-like host pool (NB_MBUF = 131072 buffers at 2176 B stride, data at
-128 B headroom, init.h:38-44); cop_process_host_stream gathers each batch's
-64-byte header lines into pinned staging, copies H2D, runs the pipeline,
+128 B headroom, init.h:38-44); cop_process_host_stream packs each batch's
+16-byte header records (COP_HDR16_STRIDE: frame bytes 12..15, 24..35) into
+pinned staging, copies H2D, runs the pipeline,
 copies the 8-byte records D2H, with the lanes overlapping; the gather runs
 on 1..16 host threads (cop_set_host_threads). Results of the first pool
 pass are checked bit-exactly against the oracle.
@@ -37,7 +38,7 @@ def main():
     ro, _, _ = orc.process(pk, NB_MBUF, stages=3, fw=o)
 
     print(f"{'lanes':>5s} {'thr':>3s} {'batch':>7s} {'Mpkt/s':>9s} {'GB/s H2D':>9s}  parity")
-    for lanes, threads in ((1, 1), (2, 1), (4, 1), (2, 4), (4, 4), (4, 8), (4, 16)):
+    for lanes, threads in ((1, 1), (2, 1), (4, 1), (2, 4), (4, 4), (2, 8), (4, 8), (2, 16), (4, 16)):
         ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=lanes)
         ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
         ctx.set_host_threads(threads)
@@ -47,7 +48,7 @@ def main():
             t0 = time.perf_counter()
             res = ctx.process_host_stream(ptrs, batch)
             dt = time.perf_counter() - t0
-            print(f"{lanes:5d} {threads:3d} {batch:7d} {n / dt / 1e6:9.1f} {n * 64 / dt / 1e9:9.2f}  "
+            print(f"{lanes:5d} {threads:3d} {batch:7d} {n / dt / 1e6:9.1f} {n * cg.HDR16_STRIDE / dt / 1e9:9.2f}  "
                   f"{'ok' if ok else 'MISMATCH'}", flush=True)
         ctx.close()
     # synchronous single-batch path (cop_process_host) for reference
