@@ -89,7 +89,11 @@ struct GatherPool {
     static void slice(const void *const *src, uint8_t *dst, uint32_t n, int parts, int i)
     {
         const uint32_t lo = (uint32_t)((uint64_t)n * i / parts), hi = (uint32_t)((uint64_t)n * (i + 1) / parts);
+        // scattered mbuf reads are DRAM-latency bound: keep PF lines in flight
+        constexpr uint32_t PF = 16;
+        for (uint32_t q = lo; q < hi && q < lo + PF; q++) __builtin_prefetch((const uint8_t *)src[q] + 12);
         for (uint32_t q = lo; q < hi; q++) {
+            if (q + PF < hi) __builtin_prefetch((const uint8_t *)src[q + PF] + 12);
             const uint8_t *p = (const uint8_t *)src[q];
             uint8_t *d = dst + (size_t)q * COP_HDR16_STRIDE;
             memcpy(d, p + 12, 4);
