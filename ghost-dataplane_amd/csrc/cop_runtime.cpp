@@ -629,12 +629,15 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
     return submit_on(c, L, batches, nb, true);
 }
 
-static int choose_ppt(const cop_ctx *c, uint64_t total)
+static int choose_ppt(const cop_ctx *c, uint64_t total, bool imix)
 {
     // tile size: the largest of 256 * {8, 4, 1} packets that still gives at
-    // least one tile per CU (fewer tiles = fewer ticket / look-back steps)
+    // least one tile per CU (fewer tiles = fewer ticket / look-back steps).
+    // IMIX stops at 4: its per-lane offset + header loads hold fewer
+    // registers per packet in flight, so more resident workgroups pay
+    // (533 vs 554 us at 384 x 64k)
     int ppt = 1;
-    if (total >= (uint64_t)COPK_BLOCK * 8 * c->ncu) ppt = 8;
+    if (total >= (uint64_t)COPK_BLOCK * 8 * c->ncu) ppt = imix ? 4 : 8;
     else if (total >= (uint64_t)COPK_BLOCK * 4 * c->ncu) ppt = 4;
     if (c->ppt_override) ppt = c->ppt_override;
     return ppt;
@@ -651,7 +654,7 @@ static Plan plan_launch(const cop_ctx *c, uint64_t total, uint32_t nb, bool imix
 {
     const bool eligible = !imix && min_stride >= COPK_STREAM_MIN_STRIDE;
     const bool hdr16 = !imix && min_stride == COP_HDR16_STRIDE;
-    Plan pl{false, choose_ppt(c, total),
+    Plan pl{false, choose_ppt(c, total, imix),
             imix    ? COPK_LAY_IMIX
             : hdr16 ? COPK_LAY_HDR16
             : (eligible && c->coalesced) ? COPK_LAY_COALESCED
