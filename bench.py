@@ -83,7 +83,7 @@ def box_ceiling(pkts_addr, n_slots, out_addr):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8192)
+    ap.add_argument("--steps", type=int, default=16384)
     ap.add_argument("--warmup", type=int, default=2048)
     ap.add_argument("--workload", default="fw1k", choices=sorted(WORKLOADS))
     ap.add_argument("--per-launch", type=int, default=0,
