@@ -92,6 +92,7 @@ def main():
     ap.add_argument("--streams", type=int, default=1, help="launch lanes (concurrent streams)")
     ap.add_argument("--pool-mib", type=int, default=0,
                     help="distinct input bytes per GPU (0: max(400 MiB, one launch of batches))")
+    ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the value is their median")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-rule-counters", action="store_true", help="ablation: config 5 without per-rule counters")
@@ -175,23 +176,31 @@ def main():
             ctx.submit_ring(ring, s % P, k)
             s += k
 
-    # ---- warmup, then exactly K timed steps ----
+    # ---- warmup, then exactly K timed steps, `repeats` times; the value is
+    # the median run (median of 5 runs) ----
     run_steps(0, args.warmup)
-    ctx.sync()
-    group.barrier()
-    ctx.sync()
-    t0 = time.perf_counter()
-    run_steps(args.warmup, args.steps)
-    if rc_on:
-        # one reporting interval: sum counters + per-rule hits over all GPUs
-        red_tot, _ = ctx.coll_reduce_counters(reset=True, with_rules=False)
-    ctx.sync()
-    t1 = time.perf_counter()
-    group.barrier()
-    elapsed = group.max(t1 - t0)
+    runs = []
+    red_tot = None
+    for r in range(max(1, args.repeats)):
+        ctx.sync()
+        group.barrier()
+        ctx.sync()
+        t0 = time.perf_counter()
+        run_steps(args.warmup + r * args.steps, args.steps)
+        if rc_on:
+            # one reporting interval: sum counters + per-rule hits over all GPUs
+            tot, _ = ctx.coll_reduce_counters(reset=True, with_rules=False)
+            if red_tot is None:
+                red_tot = tot   # the first interval also holds the warmup
+        ctx.sync()
+        t1 = time.perf_counter()
+        group.barrier()
+        runs.append(group.max(t1 - t0))
+    elapsed = float(np.median(runs))
     total_pkts = world * args.steps * B
     value = total_pkts / elapsed / 1e6
-    log(f"[rank {rank}] timed {args.steps} steps in {elapsed * 1e3:.2f} ms -> {value:.1f} Mpkt/s (all ranks)")
+    log(f"[rank {rank}] timed {args.steps} steps x {len(runs)} runs, median {elapsed * 1e3:.2f} ms "
+        f"-> {value:.1f} Mpkt/s (all ranks); runs {[round(x * 1e3, 3) for x in runs]} ms")
 
     reduce_info = None
     if rc_on:
@@ -260,6 +269,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 6),
+        "runs_ms": [round(x * 1e3, 4) for x in runs],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
