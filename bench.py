@@ -58,7 +58,7 @@ def log(*a):
 
 
 def box_ceiling(pkts_addr, n_slots, out_addr):
-    """GB/s of the 72 B/packet copy mix on this box (None if the tool is absent)."""
+    """(GB/s, pattern) of the 72 B/packet copy mix on this box (None if the tool is absent)."""
     import ctypes
 
     path = os.path.join(ROOT, "tools", "libceiling.so")
@@ -66,18 +66,21 @@ def box_ceiling(pkts_addr, n_slots, out_addr):
         log("[bench] tools/libceiling.so not built: no box ceiling")
         return None
     lib = ctypes.CDLL(path)
-    fn = lib.ceiling_copy_mix
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+    fn = lib.ceiling_pattern
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                    ctypes.POINTER(ctypes.c_float)]
     fn.restype = ctypes.c_int
-    best = None
-    for m in (4, 8, 16):
-        ms = ctypes.c_float(0.0)
-        if fn(pkts_addr, n_slots, out_addr, m, 5, ctypes.byref(ms)) == 0 and ms.value > 0:
-            best = ms.value if best is None else min(best, ms.value)
+    best, best_name = None, None
+    # grid-stride copy at 4/8/16 workgroups per CU; LDS-DMA rings at 2/3 per CU
+    for pattern, mults, name in ((0, (4, 8, 16), "grid-stride"), (1, (2, 3), "lds-dma ring")):
+        for m in mults:
+            ms = ctypes.c_float(0.0)
+            if fn(pkts_addr, n_slots, out_addr, pattern, m, 5, ctypes.byref(ms)) == 0 and ms.value > 0:
+                if best is None or ms.value < best:
+                    best, best_name = ms.value, f"{name} x{m}/CU"
     if best is None:
         return None
-    return 72.0 * n_slots / (best * 1e-3) / 1e9
+    return 72.0 * n_slots / (best * 1e-3) / 1e9, best_name
 
 
 def main():
@@ -249,9 +252,9 @@ def main():
 
     # the same box's streaming ceiling for this byte mix (tools/ceiling.hip):
     # read every 64 B slot of the pool, write an 8 B record, nothing else
-    ceiling = None
+    ceiling, ceiling_how = None, None
     if not W["imix"]:
-        ceiling = box_ceiling(d_pkts.addr, P * B, d_res.addr)
+        ceiling, ceiling_how = box_ceiling(d_pkts.addr, P * B, d_res.addr) or (None, None)
 
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_L{Lb}_s{args.streams}.json")
@@ -302,7 +305,8 @@ def main():
             "launches_timed": int(n_launch),
             "box_ceiling": (None if ceiling is None else {
                 "what": "same pool, same process: read each 64 B slot + write an 8 B record, no classification "
-                        "(tools/ceiling.hip, best of grids 4/8/16 x CUs)",
+                        "(tools/ceiling.hip: best of a grid-stride copy and per-wave LDS-DMA rings)",
+                "best_pattern": ceiling_how,
                 "achieved": round(ceiling, 2), "unit": "GB/s",
                 "frac_of_peak": round(ceiling / HBM_PEAK_GBS, 4),
                 "pipeline_frac_of_ceiling": round(achieved / ceiling, 4)}),

@@ -1,8 +1,8 @@
 // ceiling.hip — the box's streaming ceiling for the pipeline's byte mix.
 //
-// Reads every 64-byte packet slot of a pool once (coalesced non-temporal
-// 16-byte loads, grid-stride) and writes one 8-byte record per slot
-// (non-temporal): the 72 B/packet of the bench's algorithmic bytes with no
+// Reads every 64-byte packet slot of a pool once and writes one 8-byte
+// record per slot (non-temporal), in two access patterns (a grid-stride of
+// 16-byte loads; per-wave LDS-DMA rings): the 72 B/packet of the bench's algorithmic bytes with no
 // classification, no tables and no ordering. bench.py times it on the same
 // pool, in the same process, right after the pipeline, so that the
 // pipeline's roofline fraction can be read against what this box's HBM
@@ -39,12 +39,67 @@ __global__ __launch_bounds__(256) void copy_mix(const u32x4 *__restrict__ pk, u3
     }
 }
 
+// The same byte mix through per-wave LDS-DMA rings (the fastest pattern in
+// tools/membench2.hip): a persistent grid, each wave streams wave-tiles of
+// 64 slots (4 KiB, four global_load_lds_dwordx4) through a 2-deep ring in
+// LDS, keeps the next tile in flight with a counted vmcnt, reads its
+// packet's header words from LDS and writes the 8-byte record.
+__global__ __launch_bounds__(256) void ring_mix(const uint8_t *__restrict__ pk, u32x2 *__restrict__ out, uint64_t n)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr int D = 2;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t *ring = lds + wave * D * 1024;
+    const uint64_t nwt = (n + 63) / 64;
+    const uint64_t W = (uint64_t)gridDim.x * 4;
+    const uint64_t w0 = blockIdx.x * 4ull + wave;
+    auto issue = [&](uint64_t wt, int slot) {
+        uint32_t *dst = ring + slot * 1024;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const uint32_t byte = (c * 64 + lane) * 16;
+            const uint64_t q = min(wt * 64 + byte / 64, n - 1);
+            const uint8_t *src = pk + q * 64 + (byte & 63);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(dst + c * 256), 16, 0, 2);
+        }
+    };
+    const uint64_t nmine = w0 < nwt ? (nwt - w0 + W - 1) / W : 0;
+    if (nmine) issue(w0, 0);
+    for (uint64_t i = 0; i < nmine; i++) {
+        if (i + 1 < nmine) {
+            issue(w0 + (i + 1) * W, (int)((i + 1) % D));
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // tile i landed, tile i+1 in flight
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const uint32_t *buf = ring + (i % D) * 1024 + lane * 16;
+        const uint32_t w3 = buf[3], w6 = buf[6], w7 = buf[7], w8 = buf[8];
+        const uint64_t q = (w0 + i * W) * 64 + lane;
+        u32x2 r;
+        r.x = w3 ^ (w6 * 3u);
+        r.y = w7 + w8;
+        if (q < n) __builtin_nontemporal_store(r, &out[q]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the slot is refilled
+    }
+}
+
 }  // namespace
 
 // Median over `iters` launches of the copy over n_slots 64-byte slots at
 // grid = CUs * grid_mult workgroups. Returns 0 and *ms_out, or -1.
+// pattern 0: copy_mix (grid-stride 16-byte loads); 1: ring_mix (LDS-DMA rings)
+extern "C" int ceiling_pattern(const void *pkts, uint64_t n_slots, void *out, int pattern, int grid_mult, int iters,
+                               float *ms_out);
+
 extern "C" int ceiling_copy_mix(const void *pkts, uint64_t n_slots, void *out, int grid_mult, int iters,
                                 float *ms_out)
+{
+    return ceiling_pattern(pkts, n_slots, out, 0, grid_mult, iters, ms_out);
+}
+
+extern "C" int ceiling_pattern(const void *pkts, uint64_t n_slots, void *out, int pattern, int grid_mult, int iters,
+                               float *ms_out)
 {
     int dev = 0;
     hipDeviceProp_t prop;
@@ -59,7 +114,11 @@ extern "C" int ceiling_copy_mix(const void *pkts, uint64_t n_slots, void *out, i
     int rc = 0;
     for (int r = 0; r <= iters; r++) {
         (void)hipEventRecord(e0, s);
-        hipLaunchKernelGGL(copy_mix, dim3(grid), dim3(256), 0, s, (const u32x4 *)pkts, (u32x2 *)out, n_slots * 4);
+        if (pattern == 1)
+            hipLaunchKernelGGL(ring_mix, dim3(grid), dim3(256), 4 * 2 * 4096, s, (const uint8_t *)pkts, (u32x2 *)out,
+                               n_slots);
+        else
+            hipLaunchKernelGGL(copy_mix, dim3(grid), dim3(256), 0, s, (const u32x4 *)pkts, (u32x2 *)out, n_slots * 4);
         (void)hipEventRecord(e1, s);
         if (hipEventSynchronize(e1) != hipSuccess) {
             rc = -1;
