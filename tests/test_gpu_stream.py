@@ -241,3 +241,34 @@ def test_stream_rule_counters(gpu_ctx_factory):
     ro, _, _ = orc.process(pk, B * P, stages=S | F, fw=fw)
     assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
     assert int(hits.sum()) == int(np.sum((ro["flags"] & cg.FLAG_FW_HIT) != 0))
+
+
+def test_max_ring_launch_1024_slots_wrapping(gpu_ctx_factory):
+    """The bench's launch size: 1024 batches in ONE ring launch (the ticket
+    buffers' full 1024 lines, 1024 look-back chains), over a ring of 300
+    slots so the launch wraps it three times (a slot's batches in one launch
+    write identical outputs). Two launches back to back, so the second one
+    draws from the ticket buffer the first one zeroed."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    B, P = 4096 + 77, 300
+    pk = cg.gen_trace(0x5EED0A70, B * P, rules)
+    fw, _ = oracle_tables(rules)
+    ro, fos = oracle_slots(pk, B, P, S | F, fw)
+    dp = ctx.alloc(B * 64 * P)
+    dp.upload(pk)
+    dr = ctx.alloc(B * P * 8)
+    df = ctx.alloc(B * P * 4)
+    dc = ctx.alloc(P * 4)
+    dc.fill(0xFF)
+    ring = cg.make_ring(dp, P, B, dr, B * 64, stride=64, fwd_idx=df, fwd_slot=B, fwd_count=dc)
+    ctx.submit_ring(ring, 123, 1024)
+    ctx.submit_ring(ring, 7, 1024)
+    ctx.sync()
+    res = dr.download(cg.RESULT_DT, B * P)
+    fwd = df.download(np.uint32, B * P)
+    cnt = dc.download(np.uint32, P)
+    check_slots(res, fwd, cnt, ro, fos, B, range(P))
+    c = ctx.counters()
+    assert c["rx"] == 2 * 1024 * B
