@@ -256,6 +256,10 @@ def main():
     if not W["imix"]:
         ceiling, ceiling_how = box_ceiling(d_pkts.addr, P * B, d_res.addr) or (None, None)
 
+    # every GPU's own kernel rate (N > 1: the roofline line is rank 0's
+    # kernel; these give the spread and the node-wide sum against N x peak)
+    ach_min, ach_max, ach_sum = group.min(achieved), group.max(achieved), group.sum(achieved)
+
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_L{Lb}_s{args.streams}.json")
     if os.path.exists(tpath):
@@ -303,6 +307,9 @@ def main():
             "traffic_per_algorithmic": (round(traffic / alg_bytes, 4) if traffic else None),
             "kernel_ms_per_launch": round(mean_ms, 6),
             "launches_timed": int(n_launch),
+            "all_gpus": {"n": world, "achieved_sum": round(ach_sum, 2), "peak_sum": HBM_PEAK_GBS * world,
+                         "frac": round(ach_sum / (HBM_PEAK_GBS * world), 4),
+                         "per_gpu_min": round(ach_min, 2), "per_gpu_max": round(ach_max, 2)},
             "box_ceiling": (None if ceiling is None else {
                 "what": "same pool, same process: read each 64 B slot + write an 8 B record, no classification "
                         "(tools/ceiling.hip: best of a grid-stride copy and per-wave LDS-DMA rings)",

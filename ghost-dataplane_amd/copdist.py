@@ -59,6 +59,17 @@ class Group:
         self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX)
         return float(t.item())
 
+    def min(self, x: float) -> float:
+        return -self.max(-x)
+
+    def sum(self, x: float) -> float:
+        if not self._dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM)
+        return float(t.item())
+
     def sum_u64(self, a: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(a, dtype=np.uint64)
         if not self._dist:

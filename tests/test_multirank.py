@@ -29,8 +29,11 @@ uid = g.broadcast_bytes(bytes(range(128)) if rank == 0 else None)   # RCCL id di
 assert uid == bytes(range(128)), uid
 g.barrier()
 mx = g.max(float(rank + 1))
+mn = g.min(float(rank + 1))   # bench.py: per-GPU spread of the kernel rate
+sm = g.sum(float(rank + 1.5))  # bench.py: node-wide achieved GB/s
 if rank == 0:
-    print(json.dumps({"names": names, "sum": [int(x) for x in tot], "max": mx, "hits": [int(x) for x in htot]}))
+    print(json.dumps({"names": names, "sum": [int(x) for x in tot], "max": mx, "min": mn, "fsum": sm,
+                      "hits": [int(x) for x in htot]}))
 g.close()
 """
 
@@ -63,7 +66,7 @@ def test_two_rank_gloo_shards_and_reductions():
     import copgpu as cg
     import oracle as orc
     got = json.loads(outs[0][0].strip().splitlines()[-1])
-    assert got["max"] == 2.0
+    assert got["max"] == 2.0 and got["min"] == 1.0 and got["fsum"] == 4.0
     fw = cg.gen_rules(0x5EED1004, 1000, cg.GEN_FW, 20)
     lpm = orc.OracleLpm(1024, 24)
     lpm.setup(fw["ip"], fw["depth"], fw["next_hop"])
