@@ -357,10 +357,13 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
                 else if (port[k] >= p.n_ports) verdict[k] = COPK_DROP_NO_PORT;
             }
         }
+        // HBM probes only for packets that reach the coprocessor (masked-off
+        // lanes send no request); the others keep their stage-P verdict
+        const bool reach = verdict[k] == COPK_FORWARD;
         if (FW == COPK_TBL_IVT) fwe[k] = t.fw_v[eyt_search(t.fw_s, fw_lv, src[k])];
-        if (FW == COPK_TBL_DIR) fwe[k] = p.fw_tbl24[src[k] >> 8];
+        if (FW == COPK_TBL_DIR) fwe[k] = reach ? p.fw_tbl24[src[k] >> 8] : 0u;
         if (LPM == COPK_TBL_IVT) lpe[k] = t.lp_v[eyt_search(t.lp_s, lp_lv, dst[k])];
-        if (LPM == COPK_TBL_DIR) lpe[k] = p.lpm_tbl24[dst[k] >> 8];
+        if (LPM == COPK_TBL_DIR) lpe[k] = reach ? p.lpm_tbl24[dst[k] >> 8] : 0u;
     }
 }
 
