@@ -25,6 +25,9 @@ constexpr int WAVES = BLOCK / 64;
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// the same vectors at 4-byte alignment (packet fields at offsets 12 and 28)
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 

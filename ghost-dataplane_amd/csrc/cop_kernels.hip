@@ -174,11 +174,14 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
             const uint8_t *pk;
             if (IMIX) pk = B.pkts + B.offsets[ic] + B.data_off;
             else pk = B.pkts + (size_t)ic * B.stride + B.data_off;
-            w3[k] = *(const uint32_t *)(pk + 12);
-            const uint2 v67 = *(const uint2 *)(pk + 24);
-            w6[k] = v67.x;
-            w7[k] = v67.y;
-            w8[k] = *(const uint32_t *)(pk + 32);
+            // two loads: bytes 12..27 (dwordx4 at a 4-byte-aligned address;
+            // w3 and w6) and 28..35 (w7, w8)
+            const u32x4a a = *(const u32x4a *)(pk + 12);
+            const u32x2a b = *(const u32x2a *)(pk + 28);
+            w3[k] = a.x;
+            w6[k] = a.w;
+            w7[k] = b.x;
+            w8[k] = b.y;
         }
     } else {
 #pragma unroll
