@@ -159,6 +159,11 @@ SIGNATURES = {
     "process_packet": (c_int, [c_void_p]),
     "process_burst": (c_int, [c_void_p, c_uint32, c_void_p]),
     "cop_coprocessor_poll": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, POINTER(NfStats)]),
+    "cop_coprocessor_poll_async": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p,
+                                           POINTER(NfStats)]),
+    "cop_coprocessor_flush": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(NfStats)]),
+    "cop_host_batch_submit": (c_int, [c_void_p, c_uint32, c_void_p, c_uint32]),
+    "cop_host_batch_wait": (c_int, [c_void_p, c_uint32, POINTER(c_void_p), POINTER(c_uint32)]),
     "coprocessor_ctx": (c_void_p, []),
     "cop_gen_rules": (c_int, [c_uint64, c_uint32, c_int, c_uint32, c_void_p]),
     "cop_trace_opts_default": (None, [POINTER(TraceOpts)]),

@@ -203,6 +203,15 @@ struct cop_ctx {
     uint32_t *d_fwdn = nullptr;
     uint32_t stage_cap = 0;
     GatherPool *gather = nullptr;   // cop_set_host_threads
+    // asynchronous host batches (cop_host_batch_submit / _wait): slot s runs
+    // on lane s % n_lanes with its own pinned and device staging
+    struct HostSlot {
+        uint8_t *h_stage = nullptr, *d_stage = nullptr;
+        cop_result *h_res = nullptr, *d_res = nullptr;
+        uint32_t cap = 0, n = 0;
+        hipEvent_t done = nullptr;
+        bool busy = false;
+    } hs[COP_HOST_SLOTS];
     hipStream_t tele_stream = nullptr;  // cop_counters_snapshot
     uint64_t *tele_host = nullptr;
     unsigned long long *tele_dev = nullptr;
@@ -302,6 +311,13 @@ void cop_destroy(cop_ctx *c)
         if (L.d_stage) (void)hipFree(L.d_stage);
         if (L.d_res) (void)hipFree(L.d_res);
         if (L.s && L.s != c->stream) (void)hipStreamDestroy(L.s);
+    }
+    for (auto &h : c->hs) {
+        if (h.h_stage) (void)hipHostFree(h.h_stage);
+        if (h.h_res) (void)hipHostFree(h.h_res);
+        if (h.d_stage) (void)hipFree(h.d_stage);
+        if (h.d_res) (void)hipFree(h.d_res);
+        if (h.done) (void)hipEventDestroy(h.done);
     }
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->d_stage) (void)hipFree(c->d_stage);
@@ -990,6 +1006,65 @@ int cop_set_host_threads(cop_ctx *c, uint32_t n)
         if (!c->gather) return -ENOMEM;
         c->gather->start((int)n);
     }
+    return 0;
+}
+
+int cop_host_batch_submit(cop_ctx *c, uint32_t slot, const void *const *pkt_data, uint32_t n)
+{
+    if (!c || slot >= COP_HOST_SLOTS || (n && !pkt_data)) return -EINVAL;
+    if (n > c->cfg.max_batch) return set_err(c, -EINVAL, "n %u > max_batch", n);
+    auto &h = c->hs[slot];
+    if (h.busy) return set_err(c, -EBUSY, "host slot %u still in flight", slot);
+    Lane &L = c->lane[slot % (uint32_t)c->n_lanes];
+    HIPCHK(c, hipSetDevice(c->device));
+    if (h.cap < n || !h.h_stage) {
+        const uint32_t cap = n < 1024 ? 1024 : n;
+        if (h.h_stage) (void)hipHostFree(h.h_stage);
+        if (h.h_res) (void)hipHostFree(h.h_res);
+        if (h.d_stage) (void)hipFree(h.d_stage);
+        if (h.d_res) (void)hipFree(h.d_res);
+        h.h_stage = h.d_stage = nullptr;
+        h.h_res = h.d_res = nullptr;
+        h.cap = 0;
+        HIPCHK(c, hipHostMalloc(&h.h_stage, (size_t)cap * COP_HDR16_STRIDE, hipHostMallocDefault));
+        HIPCHK(c, hipHostMalloc(&h.h_res, (size_t)cap * sizeof(cop_result), hipHostMallocDefault));
+        HIPCHK(c, hipMalloc(&h.d_stage, (size_t)cap * COP_HDR16_STRIDE));
+        HIPCHK(c, hipMalloc(&h.d_res, (size_t)cap * sizeof(cop_result)));
+        h.cap = cap;
+    }
+    if (!h.done) HIPCHK(c, hipEventCreateWithFlags(&h.done, hipEventDisableTiming));
+    h.n = n;
+    if (n) {
+        // the 16-byte header records, then H2D -> pipeline -> D2H on the lane
+        host_gather(c, pkt_data, h.h_stage, n);
+        HIPCHK(c, hipMemcpyAsync(h.d_stage, h.h_stage, (size_t)n * COP_HDR16_STRIDE, hipMemcpyHostToDevice, L.s));
+        cop_batch b;
+        memset(&b, 0, sizeof(b));
+        b.pkts = h.d_stage;
+        b.n = n;
+        b.stride = COP_HDR16_STRIDE;
+        b.results = h.d_res;
+        if (int rc = submit_on(c, L, &b, 1, false)) return rc;
+        HIPCHK(c, hipMemcpyAsync(h.h_res, h.d_res, (size_t)n * sizeof(cop_result), hipMemcpyDeviceToHost, L.s));
+    }
+    HIPCHK(c, hipEventRecord(h.done, L.s));
+    h.busy = true;
+    return 0;
+}
+
+int cop_host_batch_wait(cop_ctx *c, uint32_t slot, const cop_result **results, uint32_t *n)
+{
+    if (!c || slot >= COP_HOST_SLOTS) return -EINVAL;
+    auto &h = c->hs[slot];
+    if (!h.busy) return set_err(c, -EINVAL, "host slot %u has no batch", slot);
+    HIPCHK(c, hipEventSynchronize(h.done));
+    h.busy = false;
+    if (c->h_err[0]) {
+        c->h_err[0] = 0;
+        return set_err(c, -EIO, "device reported a look-back timeout");
+    }
+    if (results) *results = h.h_res;
+    if (n) *n = h.n;
     return 0;
 }
 

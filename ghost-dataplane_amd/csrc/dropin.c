@@ -25,6 +25,17 @@ static char g_rule_file[4096] = "./nfs/firewall/rules.json"; /* coprocessor.c:19
 static int g_rule_file_set = 0;
 
 static __thread cop_ctx *tl_ctx = NULL;
+/* Pipelined ring loop: per thread, up to COP_HOST_SLOTS batches in flight,
+ * completed oldest first, so packets leave in arrival order. */
+static __thread struct {
+    void **objs[COP_HOST_SLOTS];
+    uint32_t cap[COP_HOST_SLOTS];
+    const void **data;
+    uint32_t data_cap;
+    uint32_t fifo[COP_HOST_SLOTS];   /* slots in flight, oldest first */
+    uint32_t depth;
+} tl_async;
+
 static __thread struct {
     void **objs;
     const void **data;
@@ -97,6 +108,15 @@ int coprocessor_teardown(void)
 {
     if (tl_ctx) cop_destroy(tl_ctx);
     tl_ctx = NULL;
+    for (uint32_t s = 0; s < COP_HOST_SLOTS; s++) {
+        free(tl_async.objs[s]);
+        tl_async.objs[s] = NULL;
+        tl_async.cap[s] = 0;
+    }
+    free((void *)tl_async.data);
+    tl_async.data = NULL;
+    tl_async.data_cap = 0;
+    tl_async.depth = 0;
     free(tl_buf.objs);
     free(tl_buf.data);
     free(tl_buf.res);
@@ -137,34 +157,19 @@ int process_packet(struct rte_mbuf *pkt)
     return r;
 }
 
-int cop_coprocessor_poll(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_pkts,
-                         cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats)
+/* forward in arrival order through a PKT_BURST_SZ tx buffer flushed with
+ * an all-or-nothing bulk enqueue (enqueue_nf_tx / flush_nf_tx_queue,
+ * switch.c:240-280,329-351); drops are freed (switch.c:469). */
+static void forward_batch(cop_ring *tx, void *const *objs, const cop_result *res, uint32_t n, cop_free_fn free_fn,
+                          void *free_arg, cop_nf_stats *stats)
 {
-    if (!ctx || !rx || !tx) return -EINVAL;
-    if (max_pkts == 0) max_pkts = COP_PKT_BURST_SZ;
-    if (ensure_buf(max_pkts)) return -ENOMEM;
-    /* drain rx_q in bursts of PKT_BURST_SZ (switch.c:463) */
-    uint32_t n = 0;
-    while (n < max_pkts) {
-        uint32_t want = max_pkts - n < COP_PKT_BURST_SZ ? max_pkts - n : COP_PKT_BURST_SZ;
-        uint32_t got = cop_ring_dequeue_burst(rx, tl_buf.objs + n, want, NULL);
-        n += got;
-        if (got < want) break;
-    }
-    if (n == 0) return 0;
-    for (uint32_t i = 0; i < n; i++) tl_buf.data[i] = mbuf_data((struct rte_mbuf *)tl_buf.objs[i]);
-    int rc = cop_process_host(ctx, tl_buf.data, n, tl_buf.res, NULL, NULL);
-    if (rc) return rc;
-    /* forward in arrival order through a PKT_BURST_SZ tx buffer flushed with
-     * an all-or-nothing bulk enqueue (enqueue_nf_tx / flush_nf_tx_queue,
-     * switch.c:240-280,329-351); drops are freed (switch.c:469). */
     void *txb[COP_PKT_BURST_SZ];
     uint32_t cnt = 0;
     for (uint32_t i = 0; i <= n; i++) {
         int flush = (i == n) ? cnt > 0 : 0;
         if (i < n) {
-            struct rte_mbuf *m = (struct rte_mbuf *)tl_buf.objs[i];
-            if (tl_buf.res[i].verdict == COP_FORWARD) {
+            struct rte_mbuf *m = (struct rte_mbuf *)objs[i];
+            if (res[i].verdict == COP_FORWARD) {
                 txb[cnt++] = m;
                 flush = cnt == COP_PKT_BURST_SZ;
             } else if (free_fn) {
@@ -182,5 +187,117 @@ int cop_coprocessor_poll(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_
             cnt = 0;
         }
     }
+}
+
+int cop_coprocessor_poll(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_pkts,
+                         cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats)
+{
+    if (!ctx || !rx || !tx) return -EINVAL;
+    if (max_pkts == 0) max_pkts = COP_PKT_BURST_SZ;
+    if (ensure_buf(max_pkts)) return -ENOMEM;
+    /* drain rx_q (switch.c:463 dequeues PKT_BURST_SZ per coprocessor() call;
+     * one GPU batch takes many such bursts, so dequeue POLL_BURST at a time:
+     * the same packets in the same order, fewer ring-index exchanges) */
+    enum { POLL_BURST = 8 * COP_PKT_BURST_SZ };
+    uint32_t n = 0;
+    while (n < max_pkts) {
+        uint32_t want = max_pkts - n < POLL_BURST ? max_pkts - n : POLL_BURST;
+        uint32_t got = cop_ring_dequeue_burst(rx, tl_buf.objs + n, want, NULL);
+        n += got;
+        if (got < want) break;
+    }
+    if (n == 0) return 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (i + 16 < n) __builtin_prefetch((const uint8_t *)tl_buf.objs[i + 16] + g_buf_addr_off);
+        tl_buf.data[i] = mbuf_data((struct rte_mbuf *)tl_buf.objs[i]);
+    }
+    int rc = cop_process_host(ctx, tl_buf.data, n, tl_buf.res, NULL, NULL);
+    if (rc) return rc;
+    forward_batch(tx, tl_buf.objs, tl_buf.res, n, free_fn, free_arg, stats);
     return (int)n;
+}
+
+
+
+static int async_complete_oldest(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn, void *free_arg,
+                                 cop_nf_stats *stats)
+{
+    const uint32_t s = tl_async.fifo[0];
+    const cop_result *res = NULL;
+    uint32_t n = 0;
+    int rc = cop_host_batch_wait(ctx, s, &res, &n);
+    for (uint32_t i = 1; i < tl_async.depth; i++) tl_async.fifo[i - 1] = tl_async.fifo[i];
+    tl_async.depth--;
+    if (rc) return rc;
+    forward_batch(tx, tl_async.objs[s], res, n, free_fn, free_arg, stats);
+    return (int)n;
+}
+
+int cop_coprocessor_poll_async(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_pkts,
+                               cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats)
+{
+    if (!ctx || !rx || !tx) return -EINVAL;
+    if (max_pkts == 0) max_pkts = COP_PKT_BURST_SZ;
+    int done = 0;
+    /* a free slot: complete the oldest batch if every slot is in flight */
+    if (tl_async.depth == COP_HOST_SLOTS) {
+        int r = async_complete_oldest(ctx, tx, free_fn, free_arg, stats);
+        if (r < 0) return r;
+        done += r;
+    }
+    uint32_t s = 0;
+    for (; s < COP_HOST_SLOTS; s++) {
+        int used = 0;
+        for (uint32_t i = 0; i < tl_async.depth; i++) used |= tl_async.fifo[i] == s;
+        if (!used) break;
+    }
+    if (tl_async.cap[s] < max_pkts) {
+        void **o = (void **)realloc(tl_async.objs[s], max_pkts * sizeof(void *));
+        if (!o) return -ENOMEM;
+        tl_async.objs[s] = o;
+        tl_async.cap[s] = max_pkts;
+    }
+    if (tl_async.data_cap < max_pkts) {
+        const void **d = (const void **)realloc((void *)tl_async.data, max_pkts * sizeof(void *));
+        if (!d) return -ENOMEM;
+        tl_async.data = d;
+        tl_async.data_cap = max_pkts;
+    }
+    enum { POLL_BURST = 8 * COP_PKT_BURST_SZ };
+    uint32_t n = 0;
+    while (n < max_pkts) {
+        uint32_t want = max_pkts - n < POLL_BURST ? max_pkts - n : POLL_BURST;
+        uint32_t got = cop_ring_dequeue_burst(rx, tl_async.objs[s] + n, want, NULL);
+        n += got;
+        if (got < want) break;
+    }
+    if (n) {
+        for (uint32_t i = 0; i < n; i++) {
+            if (i + 16 < n) __builtin_prefetch((const uint8_t *)tl_async.objs[s][i + 16] + g_buf_addr_off);
+            tl_async.data[i] = mbuf_data((struct rte_mbuf *)tl_async.objs[s][i]);
+        }
+        int rc = cop_host_batch_submit(ctx, s, tl_async.data, n);
+        if (rc) return rc;
+        tl_async.fifo[tl_async.depth++] = s;
+    }
+    /* complete the previous batch now (it ran while this one was gathered),
+     * or the only one in flight when rx had nothing new */
+    if (tl_async.depth > 1 || (n == 0 && tl_async.depth == 1)) {
+        int r = async_complete_oldest(ctx, tx, free_fn, free_arg, stats);
+        if (r < 0) return r;
+        done += r;
+    }
+    return done;
+}
+
+int cop_coprocessor_flush(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats)
+{
+    if (!ctx || !tx) return -EINVAL;
+    int done = 0;
+    while (tl_async.depth) {
+        int r = async_complete_oldest(ctx, tx, free_fn, free_arg, stats);
+        if (r < 0) return r;
+        done += r;
+    }
+    return done;
 }

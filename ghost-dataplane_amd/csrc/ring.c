@@ -17,9 +17,16 @@
 
 #include "cop_gpu.h"
 
+/* Each side's index and its cached copy of the other side's index share a
+ * line the other side never writes, so the two threads exchange a cache
+ * line only when the cached copy runs out (a consumer re-reads prod when it
+ * has drained what it last saw; a producer re-reads cons when it last saw
+ * the ring full), not on every call. */
 struct cop_ring {
     _Alignas(64) _Atomic uint32_t prod;  /* written by the producer */
+    uint32_t cons_seen;                  /* producer's copy of cons */
     _Alignas(64) _Atomic uint32_t cons;  /* written by the consumer */
+    uint32_t prod_seen;                  /* consumer's copy of prod */
     _Alignas(64) uint32_t size, mask, capacity;
     void **slots;
 };
@@ -53,8 +60,11 @@ void cop_ring_free(cop_ring *r)
 uint32_t cop_ring_enqueue_bulk(cop_ring *r, void *const *objs, uint32_t n, uint32_t *free_space)
 {
     uint32_t head = atomic_load_explicit(&r->prod, memory_order_relaxed);
-    uint32_t tail = atomic_load_explicit(&r->cons, memory_order_acquire);
-    uint32_t free_entries = r->capacity - (head - tail);
+    uint32_t free_entries = r->capacity - (head - r->cons_seen);
+    if (n > free_entries || free_space) {
+        r->cons_seen = atomic_load_explicit(&r->cons, memory_order_acquire);
+        free_entries = r->capacity - (head - r->cons_seen);
+    }
     if (n > free_entries) {
         if (free_space) *free_space = free_entries;
         return 0;
@@ -68,10 +78,18 @@ uint32_t cop_ring_enqueue_bulk(cop_ring *r, void *const *objs, uint32_t n, uint3
 uint32_t cop_ring_dequeue_burst(cop_ring *r, void **objs, uint32_t n, uint32_t *available)
 {
     uint32_t head = atomic_load_explicit(&r->cons, memory_order_relaxed);
-    uint32_t tail = atomic_load_explicit(&r->prod, memory_order_acquire);
-    uint32_t entries = tail - head;
+    uint32_t entries = r->prod_seen - head;
+    if (n > entries || available) {
+        r->prod_seen = atomic_load_explicit(&r->prod, memory_order_acquire);
+        entries = r->prod_seen - head;
+    }
     if (n > entries) n = entries;
-    for (uint32_t i = 0; i < n; i++) objs[i] = r->slots[(head + i) & r->mask];
+    /* slots the producer just wrote live in its core's cache: keep a few
+     * line transfers in flight instead of one per 8 pointers */
+    for (uint32_t i = 0; i < n; i++) {
+        if ((i & 7u) == 0 && i + 64 < n) __builtin_prefetch(&r->slots[(head + i + 64) & r->mask]);
+        objs[i] = r->slots[(head + i) & r->mask];
+    }
     atomic_store_explicit(&r->cons, head + n, memory_order_release);
     if (available) *available = entries - n;
     return n;

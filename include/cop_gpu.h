@@ -308,6 +308,17 @@ int  cop_process_host_stream(cop_ctx *ctx, const void *const *pkt_data, uint64_t
  * thread plus n-1 persistent workers (default 1 = the caller alone). */
 int  cop_set_host_threads(cop_ctx *ctx, uint32_t n);
 
+/* Asynchronous host batches (the building block of
+ * cop_coprocessor_poll_async): slot s < COP_HOST_SLOTS gathers the packets'
+ * 16-byte header records into its pinned staging on the calling thread, then
+ * queues H2D, the pipeline and D2H on launch lane s % n_streams and returns.
+ * cop_host_batch_wait blocks until slot s's records are in pinned host
+ * memory and points *results at them (valid until slot s is submitted
+ * again). -EBUSY if the slot is still in flight. */
+#define COP_HOST_SLOTS 2u
+int  cop_host_batch_submit(cop_ctx *ctx, uint32_t slot, const void *const *pkt_data, uint32_t n);
+int  cop_host_batch_wait(cop_ctx *ctx, uint32_t slot, const cop_result **results, uint32_t *n);
+
 /* Kernel selection (tuning; results are identical either way):
  * COP_KERNEL_AUTO (default) runs one workgroup per tile (the faster form at
  * every measured shape); STREAM uses the persistent batch-sweep kernel (one
@@ -468,6 +479,17 @@ typedef struct cop_nf_stats {
 typedef void (*cop_free_fn)(struct rte_mbuf *m, void *arg);
 int cop_coprocessor_poll(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_pkts,
                          cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats);
+/* Pipelined form of cop_coprocessor_poll: each call drains up to max_pkts
+ * and submits them as a GPU batch without waiting, then completes the
+ * previous call's batch, forwarding and freeing exactly as
+ * cop_coprocessor_poll does. So the host drains and gathers one batch while
+ * the GPU runs the other. Packets leave in arrival order. Returns packets
+ * completed by this call or -errno. When rx is empty, a call completes the
+ * batch in flight. cop_coprocessor_flush completes everything in flight
+ * (e.g. before coprocessor_teardown). */
+int cop_coprocessor_poll_async(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_pkts,
+                               cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats);
+int cop_coprocessor_flush(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats);
 /* The calling thread's context created by coprocessor_setup (or NULL). */
 cop_ctx *coprocessor_ctx(void);
 

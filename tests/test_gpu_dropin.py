@@ -114,3 +114,65 @@ def test_coprocessor_poll_rings(rules_file):
         L.cop_ring_free(tx)
     finally:
         L.coprocessor_teardown()
+
+
+@pytest.mark.parametrize("max_pkts", [512, 2048, 16384])
+def test_coprocessor_poll_async_rings(rules_file, max_pkts):
+    """The pipelined ring loop (cop_coprocessor_poll_async): a fast path that
+    keeps enqueueing between calls, batches in flight across calls, then
+    cop_coprocessor_flush. Same tx_q content and order as the oracle's
+    forward list, every drop freed exactly once."""
+    path, rules = rules_file
+    L = cg.lib()
+    L.cop_set_mbuf_layout(0, 16)
+    L.cop_set_rule_file(path.encode())
+    assert L.coprocessor_setup() == 0
+    try:
+        ctx = L.coprocessor_ctx()
+        n = 40000
+        pk = cg.gen_trace(0x5EED0610, n, rules)
+        mb = Mbufs(pk, n)
+        fwo, _ = oracle_tables(rules)
+        _, fo, _ = orc.process(pk, n, stages=3, fw=fwo)
+        rx = L.cop_ring_create(16384)
+        tx = L.cop_ring_create(65536)
+        freed = []
+        FREE = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)
+        cb = FREE(lambda m, arg: freed.append(mb.index(m)))
+        stats = cg.NfStats()
+        sent = done = 0
+        out = []
+        buf = (ctypes.c_void_p * 256)()
+        polls = 0
+        while done < n:
+            # the fast path enqueues up to 3000 packets between two polls
+            k_end = min(n, sent + 3000)
+            while sent < k_end:
+                k = min(32, k_end - sent)
+                arr = (ctypes.c_void_p * k)(*[mb.ptr(j) for j in range(sent, sent + k)])
+                if L.cop_ring_enqueue_bulk(rx, arr, k, None) != k:
+                    break
+                sent += k
+            r = L.cop_coprocessor_poll_async(ctx, rx, tx, max_pkts, cb, None, ctypes.byref(stats))
+            assert r >= 0
+            done += r
+            polls += 1
+            assert polls < 10000
+            while True:
+                k = L.cop_ring_dequeue_burst(tx, buf, 256, None)
+                if not k:
+                    break
+                out += [mb.index(buf[i]) for i in range(k)]
+        assert L.cop_coprocessor_flush(ctx, tx, cb, None, ctypes.byref(stats)) == 0
+        while True:
+            k = L.cop_ring_dequeue_burst(tx, buf, 256, None)
+            if not k:
+                break
+            out += [mb.index(buf[i]) for i in range(k)]
+        assert out == list(fo)
+        assert sorted(freed) == sorted(set(range(n)) - set(fo))
+        assert stats.tx_packets == len(fo) and stats.tx_dropped == 0
+        L.cop_ring_free(rx)
+        L.cop_ring_free(tx)
+    finally:
+        L.coprocessor_teardown()
