@@ -125,3 +125,44 @@ def test_hdr16_mixed_submit_rejected(gpu_ctx_factory):
           cg.make_batch(dp.addr + 65536, 100, dr.addr + 4096, stride=64)]
     with pytest.raises(cg.CopError):
         ctx.submit(bl)
+
+
+@pytest.mark.gpu
+def test_hdr16_with_demux_port_stats_and_rule_counters(gpu_ctx_factory):
+    """Packed records through the kernels built with the optional features
+    (EXT): per-port ordered forward lists, per-port statistics and per-rule
+    hit counters equal the oracle's on the frames."""
+    rules = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_DEMUX_PORTS | cg.CFG_PORT_STATS | cg.CFG_RULE_COUNTERS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    B, NS, P = 65536, 3, 5
+    pk = cg.gen_trace(0x5EED0C30, B * NS, rules)
+    rec = cg.pack_headers_np(pk, B * NS)
+    dp = ctx.alloc(rec.nbytes)
+    dp.upload(rec)
+    dr = ctx.alloc(B * NS * 8)
+    df = ctx.alloc(B * NS * P * 4)
+    dc = ctx.alloc(NS * P * 4)
+    rg = cg.make_ring(dp, NS, B, dr, B * 16, stride=cg.HDR16_STRIDE, fwd_idx=df, fwd_count=dc, fwd_slot=B * P)
+    ctx.submit_ring(rg, 0, NS)
+    ctx.sync()
+    res = dr.download(cg.RESULT_DT, B * NS)
+    cnt = dc.download(np.uint32, NS * P).reshape(NS, P)
+    fwd_all = df.download(np.uint32, B * NS * P)
+    fw, _ = oracle_tables(rules)
+    ro_all = []
+    for s in range(NS):
+        ro, _, _ = orc.process(pk[s * B * 64:(s + 1) * B * 64], B, stages=S | F, fw=fw)
+        ro_all.append(ro)
+        assert np.array_equal(res[s * B:(s + 1) * B].view(np.uint8), ro.view(np.uint8)), s
+        for q in range(P):
+            want = np.nonzero((ro["verdict"] == 0) & (ro["port"] == q))[0].astype(np.uint32)
+            got = fwd_all[s * B * P + q * B: s * B * P + q * B + cnt[s, q]]
+            assert np.array_equal(got, want), (s, q)
+    ro = np.concatenate(ro_all)
+    ps = ctx.port_stats()
+    for q in range(P):
+        assert ps[q]["rx_packets"] == int(np.sum(ro["port"] == q))
+        assert ps[q]["tx_packets"] == int(np.sum((ro["port"] == q) & (ro["verdict"] == 0)))
+    hits = ctx.rule_counters()
+    assert int(hits.sum()) == int(np.sum((ro["flags"] & cg.FLAG_FW_HIT) != 0))
