@@ -203,6 +203,14 @@ struct cop_ctx {
     uint32_t *d_fwdn = nullptr;
     uint32_t stage_cap = 0;
     GatherPool *gather = nullptr;   // cop_set_host_threads
+    // zero-copy form of cop_process_host for small batches: the kernel reads
+    // the header records from, and writes its records to, mapped pinned host
+    // memory (no copy-engine round trips); up to zc_max packets ($COP_ZC_MAX)
+    uint32_t zc_max = 65536;
+    uint8_t *zc_stage = nullptr;      // mapped pinned: records in
+    cop_result *zc_res = nullptr;     // mapped pinned: results out
+    uint32_t *zc_fwd = nullptr;       // mapped pinned: forward list + count
+    uint32_t zc_cap = 0;
     // asynchronous host batches (cop_host_batch_submit / _wait): slot s runs
     // on lane s % n_lanes with its own pinned and device staging
     struct HostSlot {
@@ -312,6 +320,9 @@ void cop_destroy(cop_ctx *c)
         if (L.d_res) (void)hipFree(L.d_res);
         if (L.s && L.s != c->stream) (void)hipStreamDestroy(L.s);
     }
+    if (c->zc_stage) (void)hipHostFree(c->zc_stage);
+    if (c->zc_res) (void)hipHostFree(c->zc_res);
+    if (c->zc_fwd) (void)hipHostFree(c->zc_fwd);
     for (auto &h : c->hs) {
         if (h.h_stage) (void)hipHostFree(h.h_stage);
         if (h.h_res) (void)hipHostFree(h.h_res);
@@ -425,6 +436,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     }
     if (const char *e = getenv("COP_DBG")) c->dbg = (uint32_t)strtoul(e, nullptr, 0);
     if (const char *e = getenv("COP_LDS_PAD")) c->lds_pad = (uint32_t)strtoul(e, nullptr, 0) & ~15u;
+    if (const char *e = getenv("COP_ZC_MAX")) c->zc_max = (uint32_t)strtoul(e, nullptr, 0);
     if (const char *e = getenv("COP_KERNEL")) {
         if (!strcmp(e, "oneshot")) c->kernel_mode = COP_KERNEL_ONESHOT;
         else if (!strcmp(e, "stream")) c->kernel_mode = COP_KERNEL_STREAM;
@@ -944,12 +956,56 @@ static void host_gather(cop_ctx *c, const void *const *src, uint8_t *dst, uint32
     else GatherPool::slice(src, dst, n, 1, 0);
 }
 
+// Small batches: the kernel reads the records from mapped pinned memory and
+// writes records and forward list there (one launch and one sync per call,
+// no copy-engine round trips); the CPU then copies the records out.
+static int process_host_zc(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_result *results,
+                           uint32_t *fwd_idx, uint32_t *fwd_count)
+{
+    if (c->zc_cap < n || !c->zc_stage) {
+        const uint32_t cap = n < 1024 ? 1024 : n;
+        if (c->zc_stage) (void)hipHostFree(c->zc_stage);
+        if (c->zc_res) (void)hipHostFree(c->zc_res);
+        if (c->zc_fwd) (void)hipHostFree(c->zc_fwd);
+        c->zc_stage = nullptr;
+        c->zc_res = nullptr;
+        c->zc_fwd = nullptr;
+        c->zc_cap = 0;
+        HIPCHK(c, hipHostMalloc(&c->zc_stage, (size_t)cap * COP_HDR16_STRIDE, hipHostMallocMapped));
+        HIPCHK(c, hipHostMalloc(&c->zc_res, (size_t)cap * sizeof(cop_result), hipHostMallocMapped));
+        HIPCHK(c, hipHostMalloc(&c->zc_fwd, (size_t)(cap + 4) * 4, hipHostMallocMapped));
+        c->zc_cap = cap;
+    }
+    if (int rc0 = sync_lanes(c)) return rc0;   // the mapped buffers may still be in use
+    host_gather(c, pkt_data, c->zc_stage, n);
+    void *d_stage = nullptr, *d_res = nullptr, *d_fwd = nullptr;
+    HIPCHK(c, hipHostGetDevicePointer(&d_stage, c->zc_stage, 0));
+    HIPCHK(c, hipHostGetDevicePointer(&d_res, c->zc_res, 0));
+    HIPCHK(c, hipHostGetDevicePointer(&d_fwd, c->zc_fwd, 0));
+    cop_batch b;
+    memset(&b, 0, sizeof(b));
+    b.pkts = d_stage;
+    b.n = n;
+    b.stride = COP_HDR16_STRIDE;
+    b.results = (cop_result *)d_res;
+    b.fwd_idx = fwd_idx ? (uint32_t *)d_fwd + 4 : nullptr;
+    b.fwd_count = (fwd_idx || fwd_count) ? (uint32_t *)d_fwd : nullptr;
+    if (int rc = submit_on(c, c->lane[0], &b, 1, false)) return rc;
+    if (int rc = cop_sync(c)) return rc;
+    memcpy(results, c->zc_res, (size_t)n * sizeof(cop_result));
+    const uint32_t cnt = b.fwd_count ? c->zc_fwd[0] : 0u;
+    if (fwd_idx && cnt) memcpy(fwd_idx, c->zc_fwd + 4, (size_t)cnt * 4);
+    if (fwd_count) *fwd_count = cnt;
+    return 0;
+}
+
 int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_result *results,
                      uint32_t *fwd_idx, uint32_t *fwd_count)
 {
     if (!c || (n && (!pkt_data || !results))) return -EINVAL;
     if (n > c->cfg.max_batch) return set_err(c, -EINVAL, "n %u > max_batch", n);
     HIPCHK(c, hipSetDevice(c->device));
+    if (n <= c->zc_max) return process_host_zc(c, pkt_data, n, results, fwd_idx, fwd_count);
     if (c->stage_cap < n || !c->h_stage) {
         uint32_t cap = n < 1024 ? 1024 : n;
         if (c->h_stage) (void)hipHostFree(c->h_stage);
