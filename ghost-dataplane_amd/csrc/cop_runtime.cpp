@@ -324,10 +324,8 @@ void cop_destroy(cop_ctx *c)
     if (c->zc_res) (void)hipHostFree(c->zc_res);
     if (c->zc_fwd) (void)hipHostFree(c->zc_fwd);
     for (auto &h : c->hs) {
-        if (h.h_stage) (void)hipHostFree(h.h_stage);
+        if (h.h_stage) (void)hipHostFree(h.h_stage);   // mapped: d_* alias these
         if (h.h_res) (void)hipHostFree(h.h_res);
-        if (h.d_stage) (void)hipFree(h.d_stage);
-        if (h.d_res) (void)hipFree(h.d_res);
         if (h.done) (void)hipEventDestroy(h.done);
     }
     if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -1077,23 +1075,26 @@ int cop_host_batch_submit(cop_ctx *c, uint32_t slot, const void *const *pkt_data
         const uint32_t cap = n < 1024 ? 1024 : n;
         if (h.h_stage) (void)hipHostFree(h.h_stage);
         if (h.h_res) (void)hipHostFree(h.h_res);
-        if (h.d_stage) (void)hipFree(h.d_stage);
-        if (h.d_res) (void)hipFree(h.d_res);
         h.h_stage = h.d_stage = nullptr;
         h.h_res = h.d_res = nullptr;
         h.cap = 0;
-        HIPCHK(c, hipHostMalloc(&h.h_stage, (size_t)cap * COP_HDR16_STRIDE, hipHostMallocDefault));
-        HIPCHK(c, hipHostMalloc(&h.h_res, (size_t)cap * sizeof(cop_result), hipHostMallocDefault));
-        HIPCHK(c, hipMalloc(&h.d_stage, (size_t)cap * COP_HDR16_STRIDE));
-        HIPCHK(c, hipMalloc(&h.d_res, (size_t)cap * sizeof(cop_result)));
+        // mapped pinned memory: the kernel reads the records and writes the
+        // results in host memory (no copy-engine round trips); d_* are the
+        // device's addresses of the same buffers
+        HIPCHK(c, hipHostMalloc(&h.h_stage, (size_t)cap * COP_HDR16_STRIDE, hipHostMallocMapped));
+        HIPCHK(c, hipHostMalloc(&h.h_res, (size_t)cap * sizeof(cop_result), hipHostMallocMapped));
+        void *ds = nullptr, *dr = nullptr;
+        HIPCHK(c, hipHostGetDevicePointer(&ds, h.h_stage, 0));
+        HIPCHK(c, hipHostGetDevicePointer(&dr, h.h_res, 0));
+        h.d_stage = (uint8_t *)ds;
+        h.d_res = (cop_result *)dr;
         h.cap = cap;
     }
     if (!h.done) HIPCHK(c, hipEventCreateWithFlags(&h.done, hipEventDisableTiming));
     h.n = n;
     if (n) {
-        // the 16-byte header records, then H2D -> pipeline -> D2H on the lane
+        // the 16-byte header records into mapped memory, then the pipeline
         host_gather(c, pkt_data, h.h_stage, n);
-        HIPCHK(c, hipMemcpyAsync(h.d_stage, h.h_stage, (size_t)n * COP_HDR16_STRIDE, hipMemcpyHostToDevice, L.s));
         cop_batch b;
         memset(&b, 0, sizeof(b));
         b.pkts = h.d_stage;
@@ -1101,7 +1102,6 @@ int cop_host_batch_submit(cop_ctx *c, uint32_t slot, const void *const *pkt_data
         b.stride = COP_HDR16_STRIDE;
         b.results = h.d_res;
         if (int rc = submit_on(c, L, &b, 1, false)) return rc;
-        HIPCHK(c, hipMemcpyAsync(h.h_res, h.d_res, (size_t)n * sizeof(cop_result), hipMemcpyDeviceToHost, L.s));
     }
     HIPCHK(c, hipEventRecord(h.done, L.s));
     h.busy = true;

@@ -310,8 +310,10 @@ int  cop_set_host_threads(cop_ctx *ctx, uint32_t n);
 
 /* Asynchronous host batches (the building block of
  * cop_coprocessor_poll_async): slot s < COP_HOST_SLOTS gathers the packets'
- * 16-byte header records into its pinned staging on the calling thread, then
- * queues H2D, the pipeline and D2H on launch lane s % n_streams and returns.
+ * 16-byte header records into its mapped pinned staging on the calling
+ * thread, then queues the pipeline on launch lane s % n_streams (the kernel
+ * reads the records from, and writes its results to, host memory) and
+ * returns.
  * cop_host_batch_wait blocks until slot s's records are in pinned host
  * memory and points *results at them (valid until slot s is submitted
  * again). -EBUSY if the slot is still in flight. */
