@@ -166,3 +166,34 @@ def test_hdr16_with_demux_port_stats_and_rule_counters(gpu_ctx_factory):
         assert ps[q]["tx_packets"] == int(np.sum((ro["port"] == q) & (ro["verdict"] == 0)))
     hits = ctx.rule_counters()
     assert int(hits.sum()) == int(np.sum((ro["flags"] & cg.FLAG_FW_HIT) != 0))
+
+
+@pytest.mark.gpu
+def test_host_batch_slots_submit_wait(gpu_ctx_factory):
+    """cop_host_batch_submit / _wait: two slots in flight at once on mapped
+    pinned memory, results bit-exact against the oracle, a busy slot refuses
+    a second submit (-EBUSY), an idle slot refuses a wait (-EINVAL)."""
+    import ctypes
+    rules = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
+    ctx = gpu_ctx_factory(stages=S | F)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    n = 20000
+    pk = cg.gen_trace(0x5EED0C40, 2 * n, rules)
+    pool, ptrs = scattered(pk, 2 * n)
+    fw, _ = oracle_tables(rules)
+    ro, _, _ = orc.process(pk, 2 * n, stages=S | F, fw=fw)
+    L = cg.lib()
+    p0 = ctypes.c_void_p(int(ptrs.ctypes.data))
+    p1 = ctypes.c_void_p(int(ptrs.ctypes.data) + n * 8)
+    assert L.cop_host_batch_submit(ctx.handle, 0, p0, n) == 0
+    assert L.cop_host_batch_submit(ctx.handle, 1, p1, n) == 0
+    assert L.cop_host_batch_submit(ctx.handle, 0, p0, n) == -16      # EBUSY
+    for s in (0, 1):
+        rp = ctypes.c_void_p()
+        cnt = ctypes.c_uint32()
+        assert L.cop_host_batch_wait(ctx.handle, s, ctypes.byref(rp), ctypes.byref(cnt)) == 0
+        assert cnt.value == n
+        got = np.frombuffer((ctypes.c_uint8 * (n * 8)).from_address(rp.value), dtype=cg.RESULT_DT).copy()
+        assert np.array_equal(got.view(np.uint8), ro[s * n:(s + 1) * n].view(np.uint8)), s
+    assert L.cop_host_batch_wait(ctx.handle, 0, None, None) == -22      # EINVAL: nothing in flight
+    del pool
