@@ -6,8 +6,8 @@
 //   W   write only (8 B nt record per slot)                    8 B/slot
 //   I   one-shot workgroup of 4096 slots, record written as soon as its
 //       slot is read (the pipeline's order)                   72 B/slot
-//   B   same reads, records staged in LDS (32 KiB) and written as one
-//       contiguous dwordx4 burst at the end of the workgroup   72 B/slot
+//   B   same reads, records staged in LDS (8 B x slots per workgroup) and
+//       written as one contiguous dwordx4 burst at the end   72 B/slot
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/membench3 tools/membench3.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -45,34 +45,86 @@ __global__ __launch_bounds__(256) void kW(u32x2 *__restrict__ out, uint32_t n) {
     }
 }
 
-// 4096 slots per workgroup = 16384 16-byte chunks; U chunks per lane in flight
-template <bool DEFER, int U>
+// SPW slots per workgroup = 4*SPW 16-byte chunks; U chunks per lane in flight
+template <bool DEFER, int U, int SPW = 4096>
 __global__ __launch_bounds__(256) void kB(const u32x4 *__restrict__ pk, u32x2 *__restrict__ out) {
-    __shared__ u32x2 rec[4096];
-    const uint64_t c0 = (uint64_t)blockIdx.x * 16384u;
+    __shared__ u32x2 rec[SPW];
+    const uint64_t c0 = (uint64_t)blockIdx.x * (4u * SPW);
     const uint32_t t = threadIdx.x;
-    for (uint32_t it = 0; it < 64; it += U) {
+    for (uint32_t it = 0; it < SPW / 64; it += U) {
         u32x4 v[U];
 #pragma unroll
         for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(&pk[c0 + (it + u) * 256u + t]);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t x = v[u].x ^ v[u].w;
+            const uint32_t x = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
             const uint32_t y = __shfl_xor(x, 1) + __shfl_xor(x, 2);
             const uint32_t slot = ((it + u) * 256u + t) >> 2;   // within the workgroup
             if ((t & 3) == 0) {
                 u32x2 r; r.x = x; r.y = y;
                 if (DEFER) rec[slot] = r;
-                else __builtin_nontemporal_store(r, &out[(uint64_t)blockIdx.x * 4096u + slot]);
+                else __builtin_nontemporal_store(r, &out[(uint64_t)blockIdx.x * SPW + slot]);
             }
         }
     }
     if (DEFER) {
         __syncthreads();
         const u32x4 *s = (const u32x4 *)rec;
-        u32x4 *o = (u32x4 *)(out + (uint64_t)blockIdx.x * 4096u);
+        u32x4 *o = (u32x4 *)(out + (uint64_t)blockIdx.x * SPW);
 #pragma unroll
-        for (int k = 0; k < 8; k++) __builtin_nontemporal_store(s[k * 256 + t], &o[k * 256 + t]);
+        for (int k = 0; k < SPW / 512; k++) __builtin_nontemporal_store(s[k * 256 + t], &o[k * 256 + t]);
+    }
+}
+
+// T consecutive sub-tiles of 2048 slots per workgroup; each sub-tile's
+// records staged in LDS and written as one 16 KiB burst at its end (the
+// pipeline's per-tile record burst, with T tiles per workgroup)
+template <int T, int U>
+__global__ __launch_bounds__(256) void kC(const u32x4 *__restrict__ pk, u32x2 *__restrict__ out) {
+    __shared__ u32x2 rec[2048];
+    const uint32_t t = threadIdx.x;
+    for (int st = 0; st < T; st++) {
+        const uint64_t tile = (uint64_t)blockIdx.x * T + st;
+        const uint64_t c0 = tile * 8192u;
+        for (uint32_t it = 0; it < 32; it += U) {
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(&pk[c0 + (it + u) * 256u + t]);
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t x = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+                const uint32_t y = __shfl_xor(x, 1) + __shfl_xor(x, 2);
+                const uint32_t slot = ((it + u) * 256u + t) >> 2;
+                if ((t & 3) == 0) { u32x2 r; r.x = x; r.y = y; rec[slot] = r; }
+            }
+        }
+        __syncthreads();
+        const u32x4 *s = (const u32x4 *)rec;
+        u32x4 *o = (u32x4 *)(out + tile * 2048u);
+#pragma unroll
+        for (int k = 0; k < 4; k++) __builtin_nontemporal_store(s[k * 256 + t], &o[k * 256 + t]);
+        __syncthreads();
+    }
+}
+
+// the one-shot pipeline's memory behaviour without its classification: a
+// tile of 256*PPT slots per workgroup, each lane loads its PPT slots whole
+// (4 x dwordx4), then writes their 8 B records (512 B per wave store);
+// occupancy set by dynamic LDS
+template <int PPT>
+__global__ __launch_bounds__(256) void kP(const u32x4 *__restrict__ pk, u32x2 *__restrict__ out) {
+    const uint64_t base = (uint64_t)blockIdx.x * (256u * PPT);
+    const uint32_t t = threadIdx.x;
+    u32x4 v[PPT][4];
+#pragma unroll
+    for (int k = 0; k < PPT; k++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) v[k][c] = __builtin_nontemporal_load(&pk[(base + k * 256u + t) * 4u + c]);
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        const u32x4 a = v[k][0] ^ v[k][1] ^ v[k][2] ^ v[k][3];
+        u32x2 r; r.x = a.x ^ a.y; r.y = a.z + a.w;
+        __builtin_nontemporal_store(r, &out[base + k * 256u + t]);
     }
 }
 
@@ -121,6 +173,29 @@ int main() {
     timeit("B LDS-deferred records U4", [&] { hipLaunchKernelGGL((kB<true, 4>), dim3(nwg), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
     timeit("I immediate records U8", [&] { hipLaunchKernelGGL((kB<false, 8>), dim3(nwg), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
     timeit("B LDS-deferred records U8", [&] { hipLaunchKernelGGL((kB<true, 8>), dim3(nwg), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("B deferred U4 1024 slots/WG", [&] { hipLaunchKernelGGL((kB<true, 4, 1024>), dim3(n / 1024), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("B deferred U4 2048 slots/WG", [&] { hipLaunchKernelGGL((kB<true, 4, 2048>), dim3(n / 2048), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("B deferred U4 8192 slots/WG", [&] { hipLaunchKernelGGL((kB<true, 4, 8192>), dim3(n / 8192), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("I immediate U4 2048 slots/WG", [&] { hipLaunchKernelGGL((kB<false, 4, 2048>), dim3(n / 2048), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("C 2048-tiles x1 per WG U4", [&] { hipLaunchKernelGGL((kC<1, 4>), dim3(n / 2048), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("C 2048-tiles x2 per WG U4", [&] { hipLaunchKernelGGL((kC<2, 4>), dim3(n / 4096), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("C 2048-tiles x4 per WG U4", [&] { hipLaunchKernelGGL((kC<4, 4>), dim3(n / 8192), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("C 2048-tiles x8 per WG U4", [&] { hipLaunchKernelGGL((kC<8, 4>), dim3(n / 16384), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("C 2048-tiles x4 per WG U8", [&] { hipLaunchKernelGGL((kC<4, 8>), dim3(n / 8192), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    timeit("B deferred U4 16384 slots/WG", [&] { hipLaunchKernelGGL((kB<true, 4, 16384>), dim3(n / 16384), dim3(256), 0, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    CHK(hipFuncSetAttribute((const void *)kC<4, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
+    CHK(hipFuncSetAttribute((const void *)kP<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
+    CHK(hipFuncSetAttribute((const void *)kP<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 << 10));
+    for (int lds : {36 << 10, 60 << 10}) {
+        timeit(("C 2048-tiles x4 U4 +LDS " + std::to_string(lds >> 10) + "K").c_str(), [&] {
+            hipLaunchKernelGGL((kC<4, 4>), dim3(n / 8192), dim3(256), lds, 0, (const u32x4 *)pk, out); }, 72.0 * n, 2);
+    }
+    for (int lds : {0, 20 << 10, 36 << 10, 60 << 10}) {
+        timeit(("P ppt8 one-shot +LDS " + std::to_string(lds >> 10) + "K").c_str(), [&] {
+            hipLaunchKernelGGL((kP<8>), dim3(n / 2048), dim3(256), lds, 0, (const u32x4 *)pk, out); }, 72.0 * n, 0);
+        timeit(("P ppt4 one-shot +LDS " + std::to_string(lds >> 10) + "K").c_str(), [&] {
+            hipLaunchKernelGGL((kP<4>), dim3(n / 1024), dim3(256), lds, 0, (const u32x4 *)pk, out); }, 72.0 * n, 0);
+    }
     timeit("R+W back to back g=2048", [&] {
         hipLaunchKernelGGL(kR, dim3(2048), dim3(256), 0, 0, (const u32x4 *)pk, sink, (uint64_t)n * 4);
         hipLaunchKernelGGL(kW, dim3(2048), dim3(256), 0, 0, out, n); }, 72.0 * n, 0);
