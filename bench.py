@@ -7,10 +7,15 @@ firewall ACL (1k rules), 64 B packets, batch 64k. The timed region rotates
 over a pool of distinct batches larger than the 256 MiB Infinity Cache, so
 every step reads its packets from HBM.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one
-process per GPU, each with its own context, batches and tables (the path
-shards with no data-path collective: weak scaling). A gloo barrier
-brackets the timed region and the max elapsed time over ranks is used.
+Multi-GPU: one process per GPU, each with its own context, batches and
+tables (the path shards with no data-path collective: weak scaling). A
+gloo barrier brackets the timed region and the max elapsed time over ranks
+is used. Launched either by python -m torch.distributed.run ... bench.py
+--gpus N (RANK/WORLD_SIZE set: WORLD_SIZE must equal --gpus), or as plain
+python bench.py --gpus N: the parent then spawns N rank processes with
+RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, before anything touches a GPU, and
+exits with their status (rank 0 prints the line). Every rank needs its own
+GPU: ranks that would share one are refused unless --allow-shared-gpu.
 
 Also reported (rank 0):
   roofline      algorithmic bytes per launch / mean kernel time (HIP events
@@ -23,6 +28,8 @@ Also reported (rank 0):
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -83,9 +90,45 @@ def box_ceiling(pkts_addr, n_slots, out_addr):
     return 72.0 * n_slots / (best * 1e-3) / 1e9, best_name
 
 
+def spawn_ranks(n: int) -> int:
+    """Run this script as n rank processes (one per GPU) and return their
+    worst exit status. The parent makes no GPU call: the ranks inherit its
+    stdout, where rank 0 prints the JSON line."""
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p_.wait() for p_ in procs]
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        log(f"[bench] ranks failed (rank, exit status): {bad}")
+        return max(abs(rc) for _, rc in bad) or 1
+    return 0
+
+
+def check_devices(args, world, local, ndev):
+    """One GPU per rank: refuse --gpus N ranks on fewer GPUs (they would time
+    N-way shared GPUs as N GPUs) unless --allow-shared-gpu."""
+    if world != args.gpus:
+        raise SystemExit(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: launch {args.gpus} ranks")
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if local_world > ndev and not args.allow_shared_gpu:
+        raise SystemExit(f"[bench] {local_world} ranks on this node but {ndev} GPU(s) visible: each rank needs its "
+                         f"own GPU (--allow-shared-gpu to time ranks sharing GPUs anyway)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="let more ranks than visible GPUs run (they share GPUs; the line says so)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="test the launch and rank protocol only: no GPU, fake timings (CPU tests)")
+    ap.add_argument("--dry-run-devices", type=int, default=8, help="GPUs a --dry-run pretends to see")
     ap.add_argument("--steps", type=int, default=16384)
     ap.add_argument("--warmup", type=int, default=2048)
     ap.add_argument("--workload", default="fw1k", choices=sorted(WORKLOADS))
@@ -103,13 +146,19 @@ def main():
     ap.add_argument("--no-compact", action="store_true", help="ablation: no ordered forward lists")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank, world, local = copdist.env()
     W = WORKLOADS[args.workload]
     B = W["batch"]
     Lb = max(1, args.per_launch or W["per_launch"])
 
+    if args.dry_run:
+        return dry_run(args, rank, world, local, W)
     cg.lib()   # load the HIP runtime the product links (before torch)
-    dev = copdist.device_for(local, cg.device_count())
+    ndev = cg.device_count()
+    check_devices(args, world, local, ndev)
+    dev = copdist.device_for(local, ndev)
     group = copdist.Group(rank, world, "gloo")
 
     # ---- tables (identical on every rank; packets differ per rank) ----
@@ -182,7 +231,7 @@ def main():
     # ---- warmup, then exactly K timed steps, `repeats` times; the value is
     # the median run (median of 5 runs) ----
     run_steps(0, args.warmup)
-    runs = []
+    runs, own_runs = [], []
     red_tot = None
     for r in range(max(1, args.repeats)):
         ctx.sync()
@@ -198,10 +247,14 @@ def main():
         ctx.sync()
         t1 = time.perf_counter()
         group.barrier()
+        own_runs.append(t1 - t0)
         runs.append(group.max(t1 - t0))
     elapsed = float(np.median(runs))
     total_pkts = world * args.steps * B
     value = total_pkts / elapsed / 1e6
+    # this rank's own rate (its own clock, not the max over ranks), and its device
+    own_rate = args.steps * B / float(np.median(own_runs)) / 1e6
+    ranks_info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(own_rate, 3)})
     log(f"[rank {rank}] timed {args.steps} steps x {len(runs)} runs, median {elapsed * 1e3:.2f} ms "
         f"-> {value:.1f} Mpkt/s (all ranks); runs {[round(x * 1e3, 3) for x in runs]} ms")
 
@@ -295,6 +348,7 @@ def main():
             "parallelism": f"independent per-GPU contexts x{world} (no data-path collective)",
             "pool_batches": int(P),
             "rule_counters": rc_on,
+            "ranks": ranks_info,
         },
         "roofline": {
             "bound": "hbm",
@@ -302,6 +356,10 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
+            # the timed region itself: algorithmic bytes of the K timed steps
+            # on all GPUs / the timed elapsed / (peak x GPUs) — launch, ramp,
+            # tail and host sync included (frac is the kernel steady state)
+            "frac_timed": round(bytes_per_pkt * total_pkts / elapsed / 1e9 / (HBM_PEAK_GBS * world), 4),
             "traffic": traffic,
             "algorithmic_bytes_per_pkt": round(bytes_per_pkt, 3),
             "traffic_per_algorithmic": (round(traffic / alg_bytes, 4) if traffic else None),
@@ -360,6 +418,30 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
+    group.close()
+
+
+def dry_run(args, rank, world, local, W):
+    """The launch/rank protocol with the GPU leg stubbed: device checks,
+    gloo rendezvous, barrier-bracketed fake timings, max over ranks, the
+    per-rank gather and rank 0's one JSON line (CPU tests of --gpus N)."""
+    check_devices(args, world, local, args.dry_run_devices)
+    dev = copdist.device_for(local, args.dry_run_devices)
+    group = copdist.Group(rank, world, "gloo")
+    B = W["batch"]
+    runs, own = [], []
+    for r in range(max(1, args.repeats)):
+        group.barrier()
+        t = 1e-3 * (1.0 + 0.1 * rank)   # rank r "takes" (1 + r/10) ms per run
+        own.append(t)
+        group.barrier()
+        runs.append(group.max(t))
+    elapsed = float(np.median(runs))
+    info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(args.steps * B / float(np.median(own)) / 1e6, 3)})
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(world * args.steps * B / elapsed / 1e6, 3), "unit": "Mpkt/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                          "config": {"workload": args.workload, "ranks": info}}), flush=True)
     group.close()
 
 

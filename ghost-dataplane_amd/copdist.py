@@ -79,6 +79,14 @@ class Group:
         self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM)
         return t.numpy().view(np.uint64)
 
+    def gather_obj(self, obj) -> list:
+        """Every rank's obj, in rank order, on every rank."""
+        if not self._dist:
+            return [obj]
+        out = [None] * self.world
+        self._dist.all_gather_object(out, obj)
+        return out
+
     def broadcast_bytes(self, b: bytes | None, root: int = 0) -> bytes:
         """Rank `root` passes the bytes, the others None; all get them back."""
         if not self._dist:

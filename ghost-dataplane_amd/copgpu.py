@@ -18,7 +18,6 @@ LIB_PATH = os.path.join(HERE, "libcopgpu.so")
 
 # ---------------------------------------------------------------------------
 # constants (include/cop_gpu.h)
-KERNEL_AUTO, KERNEL_ONESHOT, KERNEL_STREAM = 0, 1, 2
 STAGE_PARSE, STAGE_FW, STAGE_LPM = 0x1, 0x2, 0x4
 FORWARD, DROP_FW, DROP_PARSE, DROP_NOT_IPV4, DROP_NO_PORT = 0, 1, 2, 3, 4
 FLAG_ROUTE_HIT, FLAG_FW_HIT = 0x1, 0x2
@@ -125,7 +124,6 @@ SIGNATURES = {
     "cop_process_host_stream": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
     "cop_set_host_threads": (c_int, [c_void_p, c_uint32]),
     "cop_pack_headers": (None, [c_void_p, c_uint32, c_void_p]),
-    "cop_set_kernel_mode": (c_int, [c_void_p, c_int]),
     "cop_counters_read": (c_int, [c_void_p, c_void_p, c_int]),
     "cop_counters_device_ptr": (c_void_p, [c_void_p]),
     "cop_rule_counters_read": (c_int, [c_void_p, c_void_p, c_uint32, c_int]),
@@ -534,10 +532,6 @@ class Context:
 
     def set_host_threads(self, n: int):
         _check(lib().cop_set_host_threads(self.handle, n), self, "set_host_threads")
-
-    def set_kernel_mode(self, mode: int):
-        """KERNEL_AUTO, KERNEL_ONESHOT or KERNEL_STREAM (identical results)."""
-        _check(lib().cop_set_kernel_mode(self.handle, mode), self, "set_kernel_mode")
 
     def process_host_stream(self, ptrs: np.ndarray, batch: int) -> np.ndarray:
         """Streaming end-to-end path over host packet addresses (u64 array)."""

@@ -1,6 +1,5 @@
-// cop_device.h — device-side pieces shared by the two pipeline kernels
-// (cop_kernels.hip: one tile per workgroup; cop_stream.hip: persistent
-// streaming). Internal.
+// cop_device.h — device-side pieces of the pipeline kernels
+// (cop_kernels.hip). Internal.
 //
 // Per packet, the classification restates (SURVEY.md §8a contract):
 //   stage P   get_next_hop            switch.c:93-136  (+ fast-path drop

@@ -67,6 +67,16 @@ uint32_t cop_lpm_merged_intervals(const cop_lpm_table *t, uint32_t **starts, uin
  * tbl8: t->n_ext * 256 entries). */
 void cop_lpm_fill_dir24(const cop_lpm_table *t, uint32_t *tbl24, uint32_t *tbl8);
 
+/* Host paths with an explicit stage mask instead of the context's: the
+ * drop-in coprocessor API (dropin.c) runs the coprocessor thread's NF chain,
+ * COP_DROPIN_STAGES (process_packet, coprocessor.c:50-65). */
+int cop_process_host_stages(cop_ctx *c, uint32_t stages, const void *const *pkt_data, uint32_t n,
+                            cop_result *results, uint32_t *fwd_idx, uint32_t *fwd_count);
+/* cop_config.max_batch of a context (0 for NULL). */
+uint32_t cop_ctx_max_batch(const cop_ctx *c);
+int cop_host_batch_submit_stages(cop_ctx *c, uint32_t stages, uint32_t slot, const void *const *pkt_data,
+                                 uint32_t n);
+
 #ifdef __cplusplus
 }
 #endif

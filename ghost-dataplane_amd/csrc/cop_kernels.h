@@ -13,8 +13,7 @@
 static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_LDS_MISC_WORDS 80       /* counts, tile, prefix, counter reduction */
 #define COPK_LDS_MISC_EXT_WORDS 408  /* + per-port counts/prefixes (demux, port stats) */
-#define COPK_LDS_STREAM_MISC_WORDS 608  /* stream kernel: counter reduction, port stats, tile counts */
-#define COPK_STREAM_MIN_STRIDE 48    /* the stream kernel reads the first 48 bytes of a packet */
+#define COPK_COALESCED_MIN_STRIDE 48 /* coalesced loads move the first 48 bytes of every slot */
 #define COPK_MAX_DEMUX_PORTS 8
 #define COPK_PORT_WORDS 16           /* per shard: 8 ports x {rx, tx} */
 #define COPK_STAMP_WG 65536
@@ -109,11 +108,6 @@ extern "C" {
 // layout: COPK_LAY_*
 hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int layout, int ppt,
                        uint32_t grid, uint32_t lds_bytes, hipStream_t stream);
-// persistent batch-sweep kernel (cop_stream.hip): grid <= co-resident
-// workgroups and <= p->nb; one workgroup per batch at a time
-hipError_t copk_launch_stream(const CopKParams *p, int fw_mode, int lpm_mode, int ppt, uint32_t grid,
-                              uint32_t lds_bytes, hipStream_t stream);
-hipError_t copk_stream_occupancy(int fw_mode, int lpm_mode, int ppt, uint32_t lds_bytes, int *blocks_per_cu);
 // dst[i] = src[i] (atomic load) or atomic exchange with 0 when reset
 hipError_t copk_snapshot(unsigned long long *src, uint32_t n_words, unsigned long long *dst, int reset,
                          hipStream_t stream);

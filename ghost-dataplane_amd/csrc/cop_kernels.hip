@@ -1,6 +1,4 @@
-// cop_kernels.hip — the coprocessor NF pipeline, one-tile-per-workgroup
-// form (small launches, IMIX, strides < 48; cop_stream.hip is the persistent
-// streaming form for large launches).
+// cop_kernels.hip — the coprocessor NF pipeline, one tile per workgroup.
 //
 // One lane handles PPT packets, one workgroup one tile of 256*PPT packets.
 // Per packet the kernel restates the SURVEY.md §8a contract (cop_device.h:

@@ -164,16 +164,12 @@ struct cop_ctx {
     cop_config cfg{};
     int ncu = 256;
     int ppt_override = 0;      // $COP_PPT (1, 4, 8) for experiments; 0 = auto
-    int kernel_mode = COP_KERNEL_AUTO;   // cop_set_kernel_mode / $COP_KERNEL
-    int stream_ppt = 4;        // streaming kernel tile = 256 * stream_ppt ($COP_STREAM_PPT 1, 2, 4)
-    int stream_occ = 2;        // streaming kernel workgroups per CU, at most ($COP_STREAM_OCC)
-    uint32_t stream_min_batches = 0xFFFFFFFFu;   // auto: batch-sweep kernel from this many batches (off; $COP_STREAM_MIN_BATCHES)
-    int occ_key = -1, occ_val = 0;   // cached occupancy query
     bool coalesced = true;     // one-shot kernel: coalesced header loads where eligible ($COP_LOADS=strided: off)
     bool stage_lists = true;   // one-shot kernel: forward lists staged in LDS ($COP_STAGE_LISTS=0: off)
     uint32_t dbg = 0;          // $COP_DBG: timing-only kernel ablations
     uint32_t lds_pad = 0;      // $COP_LDS_PAD: extra LDS bytes per workgroup (occupancy experiments)
     unsigned long long *stamps = nullptr;   // dbg bit 8: per-workgroup phase stamps
+    uint32_t inject_submit = 0, inject_wait = 0;   // cop_debug_inject: failures to fake (tests)
     char err[256] = {0};
 
     uint32_t *rt_top = nullptr;
@@ -187,7 +183,9 @@ struct cop_ctx {
     unsigned long long *ctr_sum = nullptr;      // RCCL all-reduce destination
     size_t ctr_sum_words = 0;
     ncclComm_t comm = nullptr;
-    uint32_t *h_err = nullptr;                  // host-mapped
+    // host-mapped error words, one per lane (word 4*l): a look-back timeout
+    // fails only the waits on the lane whose launch timed out
+    uint32_t *h_err = nullptr;
     uint32_t *d_err = nullptr;
 
     hipEvent_t t0 = nullptr, t1 = nullptr;
@@ -243,6 +241,16 @@ static int set_err(cop_ctx *c, int code, const char *fmt, ...)
             return set_err((c), -EIO, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
                            __LINE__);                                                           \
     } while (0)
+
+// Memsets and device copies outside the launch lanes complete before they
+// return: the lanes are non-blocking streams, so a plain hipMemset (null
+// stream, asynchronous to the host) could still be zeroing look-back words
+// or counters while the next kernel on a lane uses them.
+static hipError_t memset_sync(void *p, int v, size_t bytes, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(p, v, bytes, s);
+    return e == hipSuccess ? hipStreamSynchronize(s) : e;
+}
 
 static inline uint32_t next_pow2(uint32_t x)
 {
@@ -353,10 +361,26 @@ static int upload_empty_ivt(cop_ctx *c, DevLpm &t)
     HIPCHK(c, hipMemcpy(t.vals, zero4, 16, hipMemcpyHostToDevice));
     t.m = 4;
     t.loaded = true;
+    HIPCHK(c, hipDeviceSynchronize());   // the copies have landed before any lane reads them
     return 0;
 }
 
 static int sync_lanes(cop_ctx *c);
+
+// Read and clear the device error words of the lanes in `mask`.
+static int take_lane_errors(cop_ctx *c, uint32_t mask)
+{
+    bool bad = false;
+    for (int l = 0; l < MAX_LANES; l++)
+        if ((mask >> l) & 1u) {
+            volatile uint32_t *w = c->h_err + 4 * l;
+            if (*w) {
+                *w = 0;
+                bad = true;
+            }
+        }
+    return bad ? set_err(c, -EIO, "device reported a look-back timeout") : 0;
+}
 
 int cop_set_routing_table(cop_ctx *c, const uint16_t *rt)
 {
@@ -388,6 +412,7 @@ int cop_set_routing_table(cop_ctx *c, const uint16_t *rt)
     HIPCHK(c, hipMalloc(&c->rt_leaf, nleaf ? nleaf * 512 : 16));
     if (nleaf) HIPCHK(c, hipMemcpy(c->rt_leaf, leaves.data(), nleaf * 512, hipMemcpyHostToDevice));
     c->rt_nleaf = nleaf;
+    HIPCHK(c, hipDeviceSynchronize());   // the copies have landed before any lane reads them
     return 0;
 }
 
@@ -435,21 +460,8 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_DBG")) c->dbg = (uint32_t)strtoul(e, nullptr, 0);
     if (const char *e = getenv("COP_LDS_PAD")) c->lds_pad = (uint32_t)strtoul(e, nullptr, 0) & ~15u;
     if (const char *e = getenv("COP_ZC_MAX")) c->zc_max = (uint32_t)strtoul(e, nullptr, 0);
-    if (const char *e = getenv("COP_KERNEL")) {
-        if (!strcmp(e, "oneshot")) c->kernel_mode = COP_KERNEL_ONESHOT;
-        else if (!strcmp(e, "stream")) c->kernel_mode = COP_KERNEL_STREAM;
-    }
     if (const char *e = getenv("COP_LOADS")) c->coalesced = strcmp(e, "strided") != 0;
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
-    if (const char *e = getenv("COP_STREAM_PPT")) {
-        int v = atoi(e);
-        if (v == 1 || v == 2 || v == 4) c->stream_ppt = v;
-    }
-    if (const char *e = getenv("COP_STREAM_MIN_BATCHES")) c->stream_min_batches = (uint32_t)strtoul(e, nullptr, 0);
-    if (const char *e = getenv("COP_STREAM_OCC")) {
-        int v = atoi(e);
-        if (v >= 1 && v <= 8) c->stream_occ = v;
-    }
     if (const char *e = getenv("COP_STREAMS")) {
         int v = atoi(e);
         if (v >= 1 && v <= MAX_LANES) cfg.n_streams = (uint32_t)v;
@@ -464,10 +476,10 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
         CREATE_CHK(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
         for (int q = 0; q < 2; q++) {
             CREATE_CHK(hipMalloc(&L.tickets[q], COPK_MAX_LAUNCH_BATCHES * 16 * sizeof(unsigned long long)));
-            CREATE_CHK(hipMemset(L.tickets[q], 0, COPK_MAX_LAUNCH_BATCHES * 16 * sizeof(unsigned long long)));
+            CREATE_CHK(memset_sync(L.tickets[q], 0, COPK_MAX_LAUNCH_BATCHES * 16 * sizeof(unsigned long long), L.s));
         }
         CREATE_CHK(hipMalloc(&L.look, (size_t)c->look_cap * 8));
-        CREATE_CHK(hipMemset(L.look, 0, (size_t)c->look_cap * 8));
+        CREATE_CHK(memset_sync(L.look, 0, (size_t)c->look_cap * 8, L.s));
         L.look_cap = c->look_cap;
         CREATE_CHK(hipEventCreateWithFlags(&L.join, hipEventDisableTiming));
         CREATE_CHK(hipEventCreateWithFlags(&L.done, hipEventDisableTiming));
@@ -483,9 +495,9 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     }
     c->stream = c->lane[0].s;
     CREATE_CHK(hipMalloc(&c->counters, RULE_OFF * 8));
-    CREATE_CHK(hipMemset(c->counters, 0, RULE_OFF * 8));
+    CREATE_CHK(memset_sync(c->counters, 0, RULE_OFF * 8, c->stream));
     CREATE_CHK(hipHostMalloc(&c->h_err, 64, hipHostMallocMapped));
-    c->h_err[0] = 0;
+    memset(c->h_err, 0, 64);
     CREATE_CHK(hipHostGetDevicePointer((void **)&c->d_err, c->h_err, 0));
     CREATE_CHK(hipEventCreate(&c->t0));
     CREATE_CHK(hipEventCreate(&c->t1));
@@ -571,6 +583,7 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
     HIPCHK(c, hipMemcpy(t.tbl8, h8.data(), h8.size() * 4, hipMemcpyHostToDevice));
     t.n_ext = n_ext;
     t.loaded = true;
+    HIPCHK(c, hipDeviceSynchronize());   // the copies have landed before any lane reads them
     return 0;
 }
 
@@ -580,8 +593,9 @@ static int resize_counters(cop_ctx *c, uint32_t n_rules)
 {
     unsigned long long *nb = nullptr;
     HIPCHK(c, hipMalloc(&nb, (RULE_OFF + n_rules) * 8));
-    hipError_t e = hipMemcpy(nb, c->counters, RULE_OFF * 8, hipMemcpyDeviceToDevice);
-    if (e == hipSuccess && n_rules) e = hipMemset(nb + RULE_OFF, 0, (size_t)n_rules * 8);
+    hipError_t e = hipMemcpyAsync(nb, c->counters, RULE_OFF * 8, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess && n_rules) e = hipMemsetAsync(nb + RULE_OFF, 0, (size_t)n_rules * 8, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
         (void)hipFree(nb);
         return set_err(c, -EIO, "counter resize: %s", hipGetErrorString(e));
@@ -643,7 +657,7 @@ static void harvest_one(cop_ctx *c, Lane &L)
     L.ev_count--;
 }
 
-static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb, bool demux);
+static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb, bool demux, uint32_t stages);
 static int pick_mode(const cop_ctx *c, const DevLpm &t, bool enabled, bool force_dir);
 
 int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
@@ -652,7 +666,7 @@ int cop_submit(cop_ctx *c, const cop_batch *batches, uint32_t nb)
     if (nb == 0) return 0;
     Lane &L = c->lane[c->next_lane];
     c->next_lane = (c->next_lane + 1) % c->n_lanes;
-    return submit_on(c, L, batches, nb, true);
+    return submit_on(c, L, batches, nb, true, c->cfg.stages);
 }
 
 static int choose_ppt(const cop_ctx *c, uint64_t total, bool imix)
@@ -669,46 +683,36 @@ static int choose_ppt(const cop_ctx *c, uint64_t total, bool imix)
     return ppt;
 }
 
-// Which kernel runs a launch, and its tile size (256 * ppt packets).
+// The launch's tile size (256 * ppt packets) and packet layout.
 struct Plan {
-    bool stream;
     int ppt;
-    int layout;   // one-shot kernel: COPK_LAY_*
+    int layout;   // COPK_LAY_*
 };
 
-static Plan plan_launch(const cop_ctx *c, uint64_t total, uint32_t nb, bool imix, uint32_t min_stride)
+static Plan plan_launch(const cop_ctx *c, uint64_t total, bool imix, uint32_t min_stride)
 {
-    const bool eligible = !imix && min_stride >= COPK_STREAM_MIN_STRIDE;
+    const bool wide = !imix && min_stride >= COPK_COALESCED_MIN_STRIDE;
     const bool hdr16 = !imix && min_stride == COP_HDR16_STRIDE;
-    Plan pl{false, choose_ppt(c, total, imix),
-            imix    ? COPK_LAY_IMIX
-            : hdr16 ? COPK_LAY_HDR16
-            : (eligible && c->coalesced) ? COPK_LAY_COALESCED
+    return Plan{choose_ppt(c, total, imix),
+                imix    ? COPK_LAY_IMIX
+                : hdr16 ? COPK_LAY_HDR16
+                : (wide && c->coalesced) ? COPK_LAY_COALESCED
                                          : COPK_LAY_SLOTS};
-    if (!eligible || c->kernel_mode == COP_KERNEL_ONESHOT) return pl;
-    // the batch-sweep kernel runs one workgroup per batch: worth it when
-    // there are batches for every CU and each is many tiles long
-    const uint64_t per_batch = nb ? total / nb : 0;
-    if (c->kernel_mode == COP_KERNEL_STREAM ||
-        (nb >= c->stream_min_batches && per_batch >= 16ull * COPK_BLOCK * (uint64_t)c->stream_ppt)) {
-        pl.stream = true;
-        pl.ppt = c->stream_ppt;
-    }
-    return pl;
 }
 
 // Fill the table / state part of the parameters and launch on lane L.
-// p.b / p.rg, p.nb, p.ntiles, p.uniform_ntiles and p.compact are set by the caller.
+// p.b / p.rg, p.nb, p.ntiles, p.uniform_ntiles, p.compact and p.stages are
+// set by the caller.
 static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uint32_t nb_used)
 {
     const int ppt = pl.ppt;
-    const uint32_t stages = c->cfg.stages;
+    const uint32_t stages = p.stages;
     int fw_mode = pick_mode(c, c->fw, (stages & COP_STAGE_FW) != 0, (c->cfg.flags & COP_CFG_FW_FORCE_DIR24) != 0);
     int lpm_mode =
         pick_mode(c, c->lpm, (stages & COP_STAGE_LPM) != 0, (c->cfg.flags & COP_CFG_LPM_FORCE_DIR24) != 0);
     HIPCHK(c, hipSetDevice(c->device));
-    // one chain per port (demux); the batch-sweep kernel needs none
-    const uint32_t look_need = pl.stream ? 0u : p.ntiles * (p.demux ? p.demux : 1u);
+    // one chain per port (demux)
+    const uint32_t look_need = p.ntiles * (p.demux ? p.demux : 1u);
     if (look_need > L.look_cap) {
         // grow this lane's look-back words (stream order: free after its work)
         HIPCHK(c, hipStreamSynchronize(L.s));
@@ -716,11 +720,10 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
         L.look = nullptr;
         L.look_cap = 0;
         HIPCHK(c, hipMalloc(&L.look, (size_t)look_need * 8));
-        HIPCHK(c, hipMemset(L.look, 0, (size_t)look_need * 8));
+        HIPCHK(c, memset_sync(L.look, 0, (size_t)look_need * 8, L.s));
         L.look_cap = look_need;
         L.epoch = 0;
     }
-    p.stages = stages;
     p.n_ports = c->cfg.n_ports;
     if (++L.epoch == 0) {
         HIPCHK(c, hipMemsetAsync(L.look, 0, (size_t)L.look_cap * 8, L.s));
@@ -731,6 +734,24 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     p.rt_top = c->rt_top;
     p.rt_leaf = c->rt_leaf;
     p.rt_nleaf = c->rt_nleaf;
+    // LDS carve (u32 words): rt_top 256 | leaves nleaf*128 | fw 2m | lpm 2m | misc | list stage
+    const uint32_t misc_words =
+        (p.demux || (c->cfg.flags & COP_CFG_PORT_STATS)) ? COPK_LDS_MISC_EXT_WORDS : COPK_LDS_MISC_WORDS;
+    const bool stage_list = p.compact && !p.demux && c->stage_lists;
+    auto lds_need = [&](int fwm, int lpmm) {
+        return (256u + c->rt_nleaf * 128u + (fwm == COPK_TBL_IVT ? 2u * c->fw.m : 0u) +
+                (lpmm == COPK_TBL_IVT ? 2u * c->lpm.m : 0u) + misc_words + (stage_list ? COPK_BLOCK * ppt : 0u)) *
+                   4u +
+               c->lds_pad;
+    };
+    // Too much for LDS (a dense custom routing table beside large interval
+    // tables): look the interval tables up in their DIR-24-8 images in HBM
+    // instead, the route stage's first. Results are identical.
+    while (lds_need(fw_mode, lpm_mode) > 160u * 1024u) {
+        if (lpm_mode == COPK_TBL_IVT && c->lpm.tbl24) lpm_mode = COPK_TBL_DIR;
+        else if (fw_mode == COPK_TBL_IVT && c->fw.tbl24) fw_mode = COPK_TBL_DIR;
+        else return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_need(fw_mode, lpm_mode));
+    }
     p.fw_m = fw_mode == COPK_TBL_IVT ? c->fw.m : 0;
     p.fw_starts = c->fw.starts;
     p.fw_vals = c->fw.vals;
@@ -741,22 +762,19 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     p.lpm_vals = c->lpm.vals;
     p.lpm_tbl24 = c->lpm.tbl24;
     p.lpm_tbl8 = c->lpm.tbl8;
-    // LDS carve (u32 words): rt_top 256 | leaves nleaf*128 | fw 2m | lpm 2m | misc
     uint32_t off = 256 + c->rt_nleaf * 128;
     p.lds_fw_off = off;
     off += 2 * p.fw_m;
     p.lds_lpm_off = off;
     off += 2 * p.lpm_m;
     p.lds_misc_off = off;
-    if (pl.stream) off += COPK_LDS_STREAM_MISC_WORDS;
-    else off += (p.demux || (c->cfg.flags & COP_CFG_PORT_STATS)) ? COPK_LDS_MISC_EXT_WORDS : COPK_LDS_MISC_WORDS;
+    off += misc_words;
     p.lds_stage_off = 0;
-    if (!pl.stream && p.compact && !p.demux && c->stage_lists) {
+    if (stage_list) {
         p.lds_stage_off = off;   // the tile's forward list, written out in 16-byte stores
         off += COPK_BLOCK * ppt;
     }
     const uint32_t lds_bytes = off * 4 + c->lds_pad;
-    if (lds_bytes > 160 * 1024) return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_bytes);
     // tickets: draw from buffer `parity`, zero the other buffer's dirty lines
     const int q = L.parity;
     p.tickets = L.tickets[q];
@@ -767,35 +785,19 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     p.rule_hits = (fw_mode != COPK_TBL_OFF && c->n_rule_ctr) ? c->counters + RULE_OFF : nullptr;
     p.port_ctr = c->counters + SHARD_WORDS;
     p.port_stats = (c->cfg.flags & COP_CFG_PORT_STATS) ? c->cfg.n_ports : 0u;
-    p.err = c->d_err;
+    p.err = c->d_err + 4 * (&L - c->lane);
     p.stamps = c->stamps;
     if ((c->dbg & 8u) && p.ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
-    uint32_t grid = p.ntiles;   // one-shot: one tile per workgroup
-    if (pl.stream) {
-        // persistent: no more workgroups than are co-resident, at most
-        // stream_occ per CU
-        const int key = ((fw_mode * 4 + lpm_mode) * 8 + ppt) * (160 * 1024 + 1) + (int)lds_bytes;
-        if (key != c->occ_key) {
-            int occ = 0;
-            hipError_t oe = copk_stream_occupancy(fw_mode, lpm_mode, ppt, lds_bytes, &occ);
-            if (oe != hipSuccess || occ < 1)
-                return set_err(c, -EIO, "stream kernel occupancy: %s (%d)", hipGetErrorString(oe), occ);
-            c->occ_key = key;
-            c->occ_val = occ;
-        }
-        const uint64_t resident = (uint64_t)c->ncu * (uint64_t)std::min(c->occ_val, c->stream_occ);
-        grid = (uint32_t)std::min<uint64_t>(p.nb, resident);   // one workgroup per batch at a time
-    }
+    const uint32_t grid = p.ntiles;   // one tile per workgroup
 
     if (c->timing) {
         if (L.ev_count == TIMING_SLOTS) harvest_one(c, L);
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][0], L.s));
     }
-    hipError_t e = pl.stream ? copk_launch_stream(&p, fw_mode, lpm_mode, ppt, grid, lds_bytes, L.s)
-                             : copk_launch(&p, fw_mode, lpm_mode, pl.layout, ppt, grid, lds_bytes, L.s);
+    hipError_t e = copk_launch(&p, fw_mode, lpm_mode, pl.layout, ppt, grid, lds_bytes, L.s);
     if (e != hipSuccess) return set_err(c, -EIO, "launch: %s", hipGetErrorString(e));
     L.dirty[q ^ 1] = 0;
-    L.dirty[q] = (p.compact && !(c->dbg & 2u) && !pl.stream) ? nb_used : 0;
+    L.dirty[q] = (p.compact && !(c->dbg & 2u)) ? nb_used : 0;
     L.parity = q ^ 1;
     if (c->timing) {
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][1], L.s));
@@ -806,9 +808,14 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
 }
 
 // demux: the caller's forward lists follow the COP_CFG_DEMUX_PORTS layout
-// (public submits); the library's own host paths use one list per batch
-static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb, bool demux)
+// (public submits); the library's own host paths use one list per batch.
+// stages: the context's mask, or the drop-in path's NF chain.
+static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb, bool demux, uint32_t stages)
 {
+    if (c->inject_submit) {
+        c->inject_submit--;
+        return set_err(c, -EIO, "injected submit failure");
+    }
     if (nb > c->cfg.max_batches) return set_err(c, -EINVAL, "nb %u > max_batches", nb);
     CopKParams p;
     memset(&p, 0, sizeof(p));
@@ -834,7 +841,7 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb,
     uint32_t min_stride = 0xFFFFFFFFu;
     for (uint32_t i = 0; i < nb; i++)
         if (batches[i].n) min_stride = std::min(min_stride, batches[i].stride);
-    const Plan pl = plan_launch(c, total, nb, imix, min_stride);
+    const Plan pl = plan_launch(c, total, imix, min_stride);
     const uint32_t tile = COPK_BLOCK * pl.ppt;
     uint32_t ntiles = 0;
     for (uint32_t i = 0; i < nb; i++) {
@@ -860,6 +867,7 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb,
     for (uint32_t i = 1; i < nb; i++)
         if (p.b[i].ntiles != p.b[0].ntiles) p.uniform_ntiles = 0;
     p.compact = compact ? 1u : 0u;
+    p.stages = stages;
     p.demux = (demux && compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 0u;
     return launch_on(c, L, p, imix, pl, nb);
 }
@@ -880,7 +888,7 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     const uint32_t lists = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 1u;
     if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < (uint64_t)r->n * lists))
         return set_err(c, -EINVAL, "ring: slot sizes smaller than n (x ports with demux)");
-    const Plan pl = plan_launch(c, (uint64_t)r->n * count, count, imix, r->stride);
+    const Plan pl = plan_launch(c, (uint64_t)r->n * count, imix, r->stride);
     const uint32_t tile = COPK_BLOCK * pl.ppt;
     const uint32_t tpb = r->n ? (r->n + tile - 1) / tile : 1;
     CopKParams p;
@@ -904,27 +912,18 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     p.ntiles = tpb * count;
     p.uniform_ntiles = tpb;
     p.compact = compact ? 1u : 0u;
+    p.stages = c->cfg.stages;
     p.demux = lists > 1 || (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? lists : 0u;
     Lane &L = c->lane[c->next_lane];
     c->next_lane = (c->next_lane + 1) % c->n_lanes;
     return launch_on(c, L, p, imix, pl, count);
 }
 
-int cop_set_kernel_mode(cop_ctx *c, int mode)
-{
-    if (!c || mode < COP_KERNEL_AUTO || mode > COP_KERNEL_STREAM) return -EINVAL;
-    c->kernel_mode = mode;
-    return 0;
-}
-
 int cop_sync(cop_ctx *c)
 {
     if (!c) return -EINVAL;
     if (int rc = sync_lanes(c)) return rc;
-    if (c->h_err[0]) {
-        c->h_err[0] = 0;
-        return set_err(c, -EIO, "device reported a look-back timeout");
-    }
+    if (int rc = take_lane_errors(c, 0xFu)) return rc;
     return 0;
 }
 
@@ -936,10 +935,7 @@ int cop_poll(cop_ctx *c)
         if (e == hipErrorNotReady) return -EAGAIN;
         if (e != hipSuccess) return set_err(c, -EIO, "stream: %s", hipGetErrorString(e));
     }
-    if (c->h_err[0]) {
-        c->h_err[0] = 0;
-        return set_err(c, -EIO, "device reported a look-back timeout");
-    }
+    if (int rc = take_lane_errors(c, 0xFu)) return rc;
     return 0;
 }
 
@@ -957,8 +953,8 @@ static void host_gather(cop_ctx *c, const void *const *src, uint8_t *dst, uint32
 // Small batches: the kernel reads the records from mapped pinned memory and
 // writes records and forward list there (one launch and one sync per call,
 // no copy-engine round trips); the CPU then copies the records out.
-static int process_host_zc(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_result *results,
-                           uint32_t *fwd_idx, uint32_t *fwd_count)
+static int process_host_zc(cop_ctx *c, uint32_t stages, const void *const *pkt_data, uint32_t n,
+                           cop_result *results, uint32_t *fwd_idx, uint32_t *fwd_count)
 {
     if (c->zc_cap < n || !c->zc_stage) {
         const uint32_t cap = n < 1024 ? 1024 : n;
@@ -988,7 +984,7 @@ static int process_host_zc(cop_ctx *c, const void *const *pkt_data, uint32_t n, 
     b.results = (cop_result *)d_res;
     b.fwd_idx = fwd_idx ? (uint32_t *)d_fwd + 4 : nullptr;
     b.fwd_count = (fwd_idx || fwd_count) ? (uint32_t *)d_fwd : nullptr;
-    if (int rc = submit_on(c, c->lane[0], &b, 1, false)) return rc;
+    if (int rc = submit_on(c, c->lane[0], &b, 1, false, stages)) return rc;
     if (int rc = cop_sync(c)) return rc;
     memcpy(results, c->zc_res, (size_t)n * sizeof(cop_result));
     const uint32_t cnt = b.fwd_count ? c->zc_fwd[0] : 0u;
@@ -1000,10 +996,16 @@ static int process_host_zc(cop_ctx *c, const void *const *pkt_data, uint32_t n, 
 int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_result *results,
                      uint32_t *fwd_idx, uint32_t *fwd_count)
 {
+    return cop_process_host_stages(c, c ? c->cfg.stages : 0u, pkt_data, n, results, fwd_idx, fwd_count);
+}
+
+int cop_process_host_stages(cop_ctx *c, uint32_t stages, const void *const *pkt_data, uint32_t n,
+                            cop_result *results, uint32_t *fwd_idx, uint32_t *fwd_count)
+{
     if (!c || (n && (!pkt_data || !results))) return -EINVAL;
     if (n > c->cfg.max_batch) return set_err(c, -EINVAL, "n %u > max_batch", n);
     HIPCHK(c, hipSetDevice(c->device));
-    if (n <= c->zc_max) return process_host_zc(c, pkt_data, n, results, fwd_idx, fwd_count);
+    if (n <= c->zc_max) return process_host_zc(c, stages, pkt_data, n, results, fwd_idx, fwd_count);
     if (c->stage_cap < n || !c->h_stage) {
         uint32_t cap = n < 1024 ? 1024 : n;
         if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -1036,7 +1038,7 @@ int cop_process_host(cop_ctx *c, const void *const *pkt_data, uint32_t n, cop_re
     b.results = c->d_res;
     b.fwd_idx = fwd_idx ? c->d_fwd : nullptr;
     b.fwd_count = (fwd_idx || fwd_count) ? c->d_fwdn : nullptr;
-    int rc = submit_on(c, c->lane[0], &b, 1, false);
+    int rc = submit_on(c, c->lane[0], &b, 1, false, stages);
     if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(results, c->d_res, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
     uint32_t cnt = 0;
@@ -1063,7 +1065,14 @@ int cop_set_host_threads(cop_ctx *c, uint32_t n)
     return 0;
 }
 
+uint32_t cop_ctx_max_batch(const cop_ctx *c) { return c ? c->cfg.max_batch : 0u; }
+
 int cop_host_batch_submit(cop_ctx *c, uint32_t slot, const void *const *pkt_data, uint32_t n)
+{
+    return cop_host_batch_submit_stages(c, c ? c->cfg.stages : 0u, slot, pkt_data, n);
+}
+
+int cop_host_batch_submit_stages(cop_ctx *c, uint32_t stages, uint32_t slot, const void *const *pkt_data, uint32_t n)
 {
     if (!c || slot >= COP_HOST_SLOTS || (n && !pkt_data)) return -EINVAL;
     if (n > c->cfg.max_batch) return set_err(c, -EINVAL, "n %u > max_batch", n);
@@ -1101,7 +1110,7 @@ int cop_host_batch_submit(cop_ctx *c, uint32_t slot, const void *const *pkt_data
         b.n = n;
         b.stride = COP_HDR16_STRIDE;
         b.results = h.d_res;
-        if (int rc = submit_on(c, L, &b, 1, false)) return rc;
+        if (int rc = submit_on(c, L, &b, 1, false, stages)) return rc;
     }
     HIPCHK(c, hipEventRecord(h.done, L.s));
     h.busy = true;
@@ -1113,12 +1122,15 @@ int cop_host_batch_wait(cop_ctx *c, uint32_t slot, const cop_result **results, u
     if (!c || slot >= COP_HOST_SLOTS) return -EINVAL;
     auto &h = c->hs[slot];
     if (!h.busy) return set_err(c, -EINVAL, "host slot %u has no batch", slot);
-    HIPCHK(c, hipEventSynchronize(h.done));
-    h.busy = false;
-    if (c->h_err[0]) {
-        c->h_err[0] = 0;
-        return set_err(c, -EIO, "device reported a look-back timeout");
+    hipError_t e = hipEventSynchronize(h.done);
+    if (c->inject_wait) {
+        c->inject_wait--;
+        e = hipErrorUnknown;
     }
+    h.busy = false;   // on every path: a failed wait must not wedge the slot
+    if (e != hipSuccess) return set_err(c, -EIO, "host slot %u: %s", slot, hipGetErrorString(e));
+    // only this slot's lane: another lane's timeout does not void these results
+    if (int rc = take_lane_errors(c, 1u << (slot % (uint32_t)c->n_lanes))) return rc;
     if (results) *results = h.h_res;
     if (n) *n = h.n;
     return 0;
@@ -1170,7 +1182,7 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
         b.n = k;
         b.stride = COP_HDR16_STRIDE;
         b.results = L.d_res;
-        if (int rc = submit_on(c, L, &b, 1, false)) return rc;
+        if (int rc = submit_on(c, L, &b, 1, false, c->cfg.stages)) return rc;
         HIPCHK(c, hipMemcpyAsync(L.h_res, L.d_res, (size_t)k * 8, hipMemcpyDeviceToHost, L.s));
         HIPCHK(c, hipEventRecord(L.done, L.s));
         L.busy = true;
@@ -1179,10 +1191,7 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
     }
     for (int l = 0; l < c->n_lanes; l++)
         if (int rc = lane_finish(c, c->lane[l], results)) return rc;
-    if (c->h_err[0]) {
-        c->h_err[0] = 0;
-        return set_err(c, -EIO, "device reported a look-back timeout");
-    }
+    if (int rc = take_lane_errors(c, 0xFu)) return rc;
     return 0;
 }
 
@@ -1196,7 +1205,7 @@ int cop_counters_read(cop_ctx *c, cop_counters *out, int reset)
     for (int s = 0; s < COPK_COUNTER_SHARDS; s++)
         for (int k = 0; k < COP_N_COUNTERS; k++) sum[k] += sh[(size_t)s * COP_N_COUNTERS + k];
     memcpy(out, sum, sizeof(cop_counters));
-    if (reset) HIPCHK(c, hipMemset(c->counters, 0, sh.size() * 8));
+    if (reset) HIPCHK(c, memset_sync(c->counters, 0, sh.size() * 8, c->stream));
     return 0;
 }
 
@@ -1235,7 +1244,7 @@ int cop_port_stats_read(cop_ctx *c, cop_port_stats *out, uint32_t n, int reset)
     std::vector<uint64_t> sh(PORT_WORDS);
     HIPCHK(c, hipMemcpy(sh.data(), c->counters + SHARD_WORDS, PORT_WORDS * 8, hipMemcpyDeviceToHost));
     fold_ports(sh.data(), out, n);
-    if (reset) HIPCHK(c, hipMemset(c->counters + SHARD_WORDS, 0, PORT_WORDS * 8));
+    if (reset) HIPCHK(c, memset_sync(c->counters + SHARD_WORDS, 0, PORT_WORDS * 8, c->stream));
     return (int)c->cfg.n_ports;
 }
 
@@ -1272,7 +1281,7 @@ int cop_rule_counters_read(cop_ctx *c, uint64_t *out, uint32_t cap, int reset)
     unsigned long long *d = c->counters + RULE_OFF;
     const uint32_t k = cap < c->n_rule_ctr ? cap : c->n_rule_ctr;
     if (k) HIPCHK(c, hipMemcpy(out, d, (size_t)k * 8, hipMemcpyDeviceToHost));
-    if (reset && c->n_rule_ctr) HIPCHK(c, hipMemset(d, 0, (size_t)c->n_rule_ctr * 8));
+    if (reset && c->n_rule_ctr) HIPCHK(c, memset_sync(d, 0, (size_t)c->n_rule_ctr * 8, c->stream));
     return (int)c->n_rule_ctr;
 }
 
@@ -1473,6 +1482,17 @@ int cop_timer_stop(cop_ctx *c, double *ms)
     float f = 0;
     HIPCHK(c, hipEventElapsedTime(&f, c->t0, c->t1));
     *ms = f;
+    return 0;
+}
+
+/* test hook (not in the public header): make the next `count` launches
+ * (what = 1) or host batch waits (what = 2) fail as a HIP error would, so
+ * the drop-in loops' error paths can be exercised */
+int cop_debug_inject(cop_ctx *c, int what, uint32_t count)
+{
+    if (!c || (what != 1 && what != 2)) return -EINVAL;
+    if (what == 1) c->inject_submit = count;
+    else c->inject_wait = count;
     return 0;
 }
 

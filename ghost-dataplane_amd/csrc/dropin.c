@@ -6,6 +6,11 @@
  *   process_packet       coprocessor.c:50-65  (0 forward / -1 drop)
  *   cop_coprocessor_poll switch.c:443-474     (coprocessor() loop body)
  *
+ * All of them run COP_DROPIN_STAGES, the NF chain of process_packet
+ * (fw_packet_handler, coprocessor.c:59-62): get_next_hop's parse/route
+ * drop belongs to the fast path (switch.c:406-415), which has already
+ * routed every packet it enqueues to a coprocessor ring.
+ *
  * The reference calls setup/teardown once per coprocessor lcore, five
  * threads at once (main.c:92-94, switch.c:525,537), with NF state in
  * process globals (firewall.h:107-110). Here every calling thread gets its
@@ -18,6 +23,7 @@
 #include <string.h>
 
 #include "cop_gpu.h"
+#include "cop_internal.h"
 
 static uint32_t g_buf_addr_off = 0;   /* rte_mbuf.buf_addr (DPDK 17.11-19.05) */
 static uint32_t g_data_off_off = 16;  /* rte_mbuf.data_off */
@@ -33,7 +39,9 @@ static __thread struct {
     const void **data;
     uint32_t data_cap;
     uint32_t fifo[COP_HOST_SLOTS];   /* slots in flight, oldest first */
+    uint32_t n[COP_HOST_SLOTS];      /* mbufs held by each slot in flight */
     uint32_t depth;
+    cop_ctx *ctx;                    /* the context the slots were submitted on */
 } tl_async;
 
 static __thread struct {
@@ -76,6 +84,7 @@ int coprocessor_setup(void)
     if (tl_ctx) return 0;
     cop_config cfg;
     cop_config_default(&cfg);
+    cfg.stages = COP_DROPIN_STAGES;
     const char *dev = getenv("COP_DEVICE");
     if (dev) cfg.device = atoi(dev);
     int rc = cop_create(&cfg, &tl_ctx);
@@ -104,8 +113,33 @@ int coprocessor_setup(void)
     return 0;
 }
 
+/* Free n dequeued mbufs that will never be forwarded (an error after the
+ * dequeue): the reference never loses a dequeued packet, it enqueues or
+ * frees each one (switch.c:464-470). Counted as tx_dropped. */
+static void drop_all(void *const *objs, uint32_t n, cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats)
+{
+    if (free_fn)
+        for (uint32_t i = 0; i < n; i++) free_fn((struct rte_mbuf *)objs[i], free_arg);
+    if (stats) stats->tx_dropped += n;
+}
+
 int coprocessor_teardown(void)
 {
+    int rc = 0;
+    if (tl_async.depth) {
+        /* batches still in flight (cop_coprocessor_flush was not called):
+         * wait for their kernels before the context goes away; their mbufs
+         * were never forwarded or freed, so say so */
+        uint32_t held = 0;
+        for (uint32_t i = 0; i < tl_async.depth; i++) {
+            (void)cop_host_batch_wait(tl_async.ctx, tl_async.fifo[i], NULL, NULL);
+            held += tl_async.n[tl_async.fifo[i]];
+        }
+        fprintf(stderr, "coprocessor_teardown: %u batch(es) in flight, %u mbufs neither forwarded nor freed "
+                        "(call cop_coprocessor_flush first)\n", tl_async.depth, held);
+        tl_async.depth = 0;
+        rc = 1;
+    }
     if (tl_ctx) cop_destroy(tl_ctx);
     tl_ctx = NULL;
     for (uint32_t s = 0; s < COP_HOST_SLOTS; s++) {
@@ -116,12 +150,12 @@ int coprocessor_teardown(void)
     free((void *)tl_async.data);
     tl_async.data = NULL;
     tl_async.data_cap = 0;
-    tl_async.depth = 0;
+    tl_async.ctx = NULL;
     free(tl_buf.objs);
     free(tl_buf.data);
     free(tl_buf.res);
     memset(&tl_buf, 0, sizeof(tl_buf));
-    return 0;
+    return rc;
 }
 
 static int ensure_buf(uint32_t n)
@@ -144,7 +178,7 @@ int process_burst(struct rte_mbuf **pkts, uint32_t n, int *ret)
     if (!tl_ctx || (n && (!pkts || !ret))) return -EINVAL;
     if (ensure_buf(n)) return -ENOMEM;
     for (uint32_t i = 0; i < n; i++) tl_buf.data[i] = mbuf_data(pkts[i]);
-    int rc = cop_process_host(tl_ctx, tl_buf.data, n, tl_buf.res, NULL, NULL);
+    int rc = cop_process_host_stages(tl_ctx, COP_DROPIN_STAGES, tl_buf.data, n, tl_buf.res, NULL, NULL);
     if (rc) return rc;
     for (uint32_t i = 0; i < n; i++) ret[i] = tl_buf.res[i].verdict == COP_FORWARD ? 0 : -1;
     return 0;
@@ -189,35 +223,46 @@ static void forward_batch(cop_ring *tx, void *const *objs, const cop_result *res
     }
 }
 
+/* dequeue up to max_pkts from rx (switch.c:463 dequeues PKT_BURST_SZ per
+ * coprocessor() call; one GPU batch takes many such bursts, so dequeue
+ * POLL_BURST at a time: the same packets in the same order, fewer
+ * ring-index exchanges) and resolve each mbuf's data address */
+static uint32_t drain_rx(cop_ring *rx, void **objs, const void **data, uint32_t max_pkts)
+{
+    enum { POLL_BURST = 8 * COP_PKT_BURST_SZ };
+    uint32_t n = 0;
+    while (n < max_pkts) {
+        uint32_t want = max_pkts - n < POLL_BURST ? max_pkts - n : POLL_BURST;
+        uint32_t got = cop_ring_dequeue_burst(rx, objs + n, want, NULL);
+        n += got;
+        if (got < want) break;
+    }
+    for (uint32_t i = 0; i < n; i++) {
+        if (i + 16 < n) __builtin_prefetch((const uint8_t *)objs[i + 16] + g_buf_addr_off);
+        data[i] = mbuf_data((struct rte_mbuf *)objs[i]);
+    }
+    return n;
+}
+
 int cop_coprocessor_poll(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_pkts,
                          cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats)
 {
     if (!ctx || !rx || !tx) return -EINVAL;
     if (max_pkts == 0) max_pkts = COP_PKT_BURST_SZ;
+    /* refuse before dequeuing anything: a batch the context cannot take
+     * would strand every mbuf it dequeued */
+    if (max_pkts > cop_ctx_max_batch(ctx)) return -EINVAL;
     if (ensure_buf(max_pkts)) return -ENOMEM;
-    /* drain rx_q (switch.c:463 dequeues PKT_BURST_SZ per coprocessor() call;
-     * one GPU batch takes many such bursts, so dequeue POLL_BURST at a time:
-     * the same packets in the same order, fewer ring-index exchanges) */
-    enum { POLL_BURST = 8 * COP_PKT_BURST_SZ };
-    uint32_t n = 0;
-    while (n < max_pkts) {
-        uint32_t want = max_pkts - n < POLL_BURST ? max_pkts - n : POLL_BURST;
-        uint32_t got = cop_ring_dequeue_burst(rx, tl_buf.objs + n, want, NULL);
-        n += got;
-        if (got < want) break;
-    }
+    const uint32_t n = drain_rx(rx, tl_buf.objs, tl_buf.data, max_pkts);
     if (n == 0) return 0;
-    for (uint32_t i = 0; i < n; i++) {
-        if (i + 16 < n) __builtin_prefetch((const uint8_t *)tl_buf.objs[i + 16] + g_buf_addr_off);
-        tl_buf.data[i] = mbuf_data((struct rte_mbuf *)tl_buf.objs[i]);
+    int rc = cop_process_host_stages(ctx, COP_DROPIN_STAGES, tl_buf.data, n, tl_buf.res, NULL, NULL);
+    if (rc) {
+        drop_all(tl_buf.objs, n, free_fn, free_arg, stats);
+        return rc;
     }
-    int rc = cop_process_host(ctx, tl_buf.data, n, tl_buf.res, NULL, NULL);
-    if (rc) return rc;
     forward_batch(tx, tl_buf.objs, tl_buf.res, n, free_fn, free_arg, stats);
     return (int)n;
 }
-
-
 
 static int async_complete_oldest(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn, void *free_arg,
                                  cop_nf_stats *stats)
@@ -228,8 +273,14 @@ static int async_complete_oldest(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn
     int rc = cop_host_batch_wait(ctx, s, &res, &n);
     for (uint32_t i = 1; i < tl_async.depth; i++) tl_async.fifo[i - 1] = tl_async.fifo[i];
     tl_async.depth--;
-    if (rc) return rc;
+    if (rc) {
+        /* no verdicts for this batch: its mbufs are freed, never leaked */
+        drop_all(tl_async.objs[s], tl_async.n[s], free_fn, free_arg, stats);
+        tl_async.n[s] = 0;
+        return rc;
+    }
     forward_batch(tx, tl_async.objs[s], res, n, free_fn, free_arg, stats);
+    tl_async.n[s] = 0;
     return (int)n;
 }
 
@@ -238,6 +289,8 @@ int cop_coprocessor_poll_async(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_
 {
     if (!ctx || !rx || !tx) return -EINVAL;
     if (max_pkts == 0) max_pkts = COP_PKT_BURST_SZ;
+    if (max_pkts > cop_ctx_max_batch(ctx)) return -EINVAL;   /* before any dequeue */
+    if (tl_async.depth && tl_async.ctx != ctx) return -EBUSY; /* flush the other context first */
     int done = 0;
     /* a free slot: complete the oldest batch if every slot is in flight */
     if (tl_async.depth == COP_HOST_SLOTS) {
@@ -263,21 +316,15 @@ int cop_coprocessor_poll_async(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_
         tl_async.data = d;
         tl_async.data_cap = max_pkts;
     }
-    enum { POLL_BURST = 8 * COP_PKT_BURST_SZ };
-    uint32_t n = 0;
-    while (n < max_pkts) {
-        uint32_t want = max_pkts - n < POLL_BURST ? max_pkts - n : POLL_BURST;
-        uint32_t got = cop_ring_dequeue_burst(rx, tl_async.objs[s] + n, want, NULL);
-        n += got;
-        if (got < want) break;
-    }
+    const uint32_t n = drain_rx(rx, tl_async.objs[s], tl_async.data, max_pkts);
     if (n) {
-        for (uint32_t i = 0; i < n; i++) {
-            if (i + 16 < n) __builtin_prefetch((const uint8_t *)tl_async.objs[s][i + 16] + g_buf_addr_off);
-            tl_async.data[i] = mbuf_data((struct rte_mbuf *)tl_async.objs[s][i]);
+        int rc = cop_host_batch_submit_stages(ctx, COP_DROPIN_STAGES, s, tl_async.data, n);
+        if (rc) {
+            drop_all(tl_async.objs[s], n, free_fn, free_arg, stats);
+            return rc;
         }
-        int rc = cop_host_batch_submit(ctx, s, tl_async.data, n);
-        if (rc) return rc;
+        tl_async.n[s] = n;
+        tl_async.ctx = ctx;
         tl_async.fifo[tl_async.depth++] = s;
     }
     /* complete the previous batch now (it ran while this one was gathered),
@@ -293,11 +340,15 @@ int cop_coprocessor_poll_async(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_
 int cop_coprocessor_flush(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats)
 {
     if (!ctx || !tx) return -EINVAL;
-    int done = 0;
+    if (tl_async.depth && tl_async.ctx != ctx) return -EINVAL;
+    int done = 0, err = 0;
     while (tl_async.depth) {
         int r = async_complete_oldest(ctx, tx, free_fn, free_arg, stats);
-        if (r < 0) return r;
+        if (r < 0) {
+            if (!err) err = r;   /* keep completing: every held mbuf is forwarded or freed */
+            continue;
+        }
         done += r;
     }
-    return done;
+    return err ? err : done;
 }

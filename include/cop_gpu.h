@@ -57,6 +57,17 @@ extern "C" {
 #define COP_DEFAULT_STAGES (COP_STAGE_PARSE | COP_STAGE_FW)
 #endif
 
+/* Stages of the drop-in coprocessor API (process_packet, process_burst,
+ * cop_coprocessor_poll*): the coprocessor thread's NF chain only —
+ * process_packet runs fw_packet_handler under ENABLE_FW_NF
+ * (coprocessor.c:59-62), which coprocessor.h:21 always defines. Parse and
+ * vport routing (get_next_hop, the UNKNOWN_PORT drop) are the fast path's
+ * job before a packet is enqueued to the coprocessor (switch.c:406-415),
+ * so the drop-in never drops on them: an IPv4 packet whose dst&0xFFFF is in
+ * 0..4, or an IPv6 EtherType, gets the firewall's verdict. The batch API
+ * (cop_submit*, cop_process_host*) runs cop_config.stages. */
+#define COP_DROPIN_STAGES (COP_STAGE_FW)
+
 /* Per-packet verdicts (one byte of the result record).
  *   FORWARD/DROP_FW : enum FW_ACTION firewall.h:71-74 (FW_FORWARD=0, FW_DROP=1)
  *   DROP_PARSE      : get_next_hop() == UNKNOWN_PORT, freed by the fast path
@@ -320,17 +331,6 @@ int  cop_set_host_threads(cop_ctx *ctx, uint32_t n);
 #define COP_HOST_SLOTS 2u
 int  cop_host_batch_submit(cop_ctx *ctx, uint32_t slot, const void *const *pkt_data, uint32_t n);
 int  cop_host_batch_wait(cop_ctx *ctx, uint32_t slot, const cop_result **results, uint32_t *n);
-
-/* Kernel selection (tuning; results are identical either way):
- * COP_KERNEL_AUTO (default) runs one workgroup per tile (the faster form at
- * every measured shape); STREAM uses the persistent batch-sweep kernel (one
- * workgroup sweeps a whole batch) whenever the launch is eligible (packet
- * batches at stride >= 48, no IMIX offsets); ONESHOT never.
- * Also $COP_KERNEL = auto | oneshot | stream. */
-#define COP_KERNEL_AUTO    0
-#define COP_KERNEL_ONESHOT 1
-#define COP_KERNEL_STREAM  2
-int  cop_set_kernel_mode(cop_ctx *ctx, int mode);
 
 /* Counters (u64, device-resident, summed over every submitted packet).
  * On the device they are kept in COP_COUNTER_SHARDS shards of

@@ -30,28 +30,17 @@ def _ensure_built():
 _ensure_built()
 
 
-@pytest.fixture(params=["auto", "stream"])
-def kernel_mode(request):
-    """Every GPU test runs twice: with the library's own kernel choice (small
-    launches take the one-tile-per-workgroup kernel) and with the persistent
-    streaming kernel forced wherever the launch is eligible. Both must give
-    the same bit-exact results."""
-    return request.param
-
-
 @pytest.fixture
-def gpu_ctx_factory(kernel_mode):
+def gpu_ctx_factory():
     import copgpu as cg
 
     if cg.device_count() < 1:
         pytest.fail("GPU test on a machine without a visible GPU")
     made = []
-    mode = {"auto": cg.KERNEL_AUTO, "stream": cg.KERNEL_STREAM}[kernel_mode]
 
     def make(**kw):
         c = cg.Context(**kw)
         made.append(c)
-        c.set_kernel_mode(mode)
         return c
 
     yield make

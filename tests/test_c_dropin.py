@@ -57,7 +57,10 @@ def test_c_dropin_matches_oracle(tmp_path):
     pk = cg.gen_trace(0x5EED0C00, n, loaded)
     o = orc.OracleLpm(1024, 24)
     o.setup(loaded["ip"], loaded["depth"], loaded["next_hop"])
-    ro, fo, _ = orc.process(pk, n, stages=cg.STAGE_PARSE | cg.STAGE_FW, fw=o)
+    # the drop-in runs the FW chain only (COP_DROPIN_STAGES, coprocessor.c:59-62)
+    ro, fo, _ = orc.process(pk, n, stages=cg.STAGE_FW, fw=o)
+    rp, _, _ = orc.process(pk, n, stages=cg.STAGE_PARSE | cg.STAGE_FW, fw=o)
+    assert np.sum((rp["verdict"] == cg.DROP_PARSE) & (ro["verdict"] == 0)) > 0
     want = np.where(ro["verdict"] == 0, 0, -1).astype(np.int32)
     assert np.array_equal(ret1, want[:n1])
     assert np.array_equal(ret2, want)

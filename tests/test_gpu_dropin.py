@@ -1,7 +1,15 @@
 """Drop-in coprocessor API on the GPU: coprocessor_setup / process_packet /
 process_burst (coprocessor.c:21-65) with rte_mbuf-shaped descriptors, and
 cop_coprocessor_poll, the GPU form of one coprocessor() call
-(switch.c:443-474), over rte_ring-semantics rings."""
+(switch.c:443-474), over rte_ring-semantics rings.
+
+The drop-in runs the coprocessor's NF chain only (COP_DROPIN_STAGES = FW:
+process_packet -> fw_packet_handler, coprocessor.c:59-62); get_next_hop's
+drop of UNKNOWN destinations and non-IPv4 EtherTypes is the fast path's
+(switch.c:406-415). The traces hold both kinds of packet (5 % dst&0xFFFF in
+0..4, 2 % EtherType 0x86DD), so the oracle they are checked against is the
+FW-only chain, and the tests assert that it differs from the P+FW batch
+pipeline on them."""
 import ctypes
 import os
 
@@ -16,6 +24,7 @@ pytestmark = pytest.mark.gpu
 
 HEADROOM = 128
 STRIDE = 2176   # MBUF_DATA_SZ, init.h:38-41
+DROPIN = cg.STAGE_FW   # COP_DROPIN_STAGES
 
 
 class Mbufs:
@@ -58,8 +67,11 @@ def test_setup_process_packet_and_burst(rules_file):
         pk = cg.gen_trace(0x5EED0500, n, rules)
         mb = Mbufs(pk, n)
         fwo, _ = oracle_tables(rules)
-        ro, _, _ = orc.process(pk, n, stages=3, fw=fwo)
+        ro, _, _ = orc.process(pk, n, stages=DROPIN, fw=fwo)
         want = np.where(ro["verdict"] == 0, 0, -1)
+        rp, _, _ = orc.process(pk, n, stages=cg.STAGE_PARSE | cg.STAGE_FW, fw=fwo)
+        # packets get_next_hop would drop but the firewall forwards
+        assert np.sum((rp["verdict"] == cg.DROP_PARSE) & (ro["verdict"] == 0)) > 0
         for i in range(0, n, 97):
             assert L.process_packet(ctypes.c_void_p(mb.ptr(i))) == want[i], i
         ptrs = (ctypes.c_void_p * n)(*[mb.ptr(i) for i in range(n)])
@@ -83,7 +95,7 @@ def test_coprocessor_poll_rings(rules_file):
         pk = cg.gen_trace(0x5EED0600, n, rules)
         mb = Mbufs(pk, n)
         fwo, _ = oracle_tables(rules)
-        ro, fo, _ = orc.process(pk, n, stages=3, fw=fwo)
+        ro, fo, _ = orc.process(pk, n, stages=DROPIN, fw=fwo)
         rx = L.cop_ring_create(16384)
         tx = L.cop_ring_create(16384)
         freed = []
@@ -133,7 +145,7 @@ def test_coprocessor_poll_async_rings(rules_file, max_pkts):
         pk = cg.gen_trace(0x5EED0610, n, rules)
         mb = Mbufs(pk, n)
         fwo, _ = oracle_tables(rules)
-        _, fo, _ = orc.process(pk, n, stages=3, fw=fwo)
+        _, fo, _ = orc.process(pk, n, stages=DROPIN, fw=fwo)
         rx = L.cop_ring_create(16384)
         tx = L.cop_ring_create(65536)
         freed = []
@@ -172,6 +184,135 @@ def test_coprocessor_poll_async_rings(rules_file, max_pkts):
         assert out == list(fo)
         assert sorted(freed) == sorted(set(range(n)) - set(fo))
         assert stats.tx_packets == len(fo) and stats.tx_dropped == 0
+        L.cop_ring_free(rx)
+        L.cop_ring_free(tx)
+    finally:
+        L.coprocessor_teardown()
+
+
+def unrouted_packet(src_ip, dst_low16, ethertype=0x0800):
+    """One 64 B UDP/IPv4 frame whose destination get_next_hop would drop
+    (routing_table[dst & 0xFFFF] == UNKNOWN_PORT for 0..4, init.c:51-53)."""
+    f = np.zeros(64, np.uint8)
+    f[12:14] = [ethertype >> 8, ethertype & 0xFF]
+    f[14] = 0x45
+    f[23] = 17
+    f[26:30] = np.frombuffer(np.uint32(src_ip).byteswap().tobytes(), np.uint8)
+    f[30:34] = np.frombuffer(np.uint32((0xC0A70000 | dst_low16)).byteswap().tobytes(), np.uint8)
+    return f
+
+
+def test_process_packet_unrouted_ipv4_gets_firewall_verdict(tmp_path):
+    """process_packet on IPv4 packets with dst&0xFFFF in {0..4}, and on
+    EtherType 0x86DD with an IPv4 header behind it: the reference's
+    process_packet returns fw_packet_handler's verdict for them (it never
+    looks at the route), so a source inside an action-0 rule forwards (0) and
+    one inside a non-zero rule drops (-1)."""
+    rules = np.zeros(2, dtype=cg.PREFIX_DT)
+    rules["ip"] = [0x0A000000, 0x0B000000]
+    rules["depth"] = [8, 8]
+    rules["next_hop"] = [0, 7]
+    f = tmp_path / "rules.json"
+    cg.rules_write_json(str(f), rules)
+    L = cg.lib()
+    L.cop_set_mbuf_layout(0, 16)
+    L.cop_set_rule_file(str(f).encode())
+    assert L.coprocessor_setup() == 0
+    try:
+        frames, want = [], []
+        for low in range(5):
+            frames.append(unrouted_packet(0x0A010203, low)); want.append(0)
+            frames.append(unrouted_packet(0x0B010203, low)); want.append(-1)
+            frames.append(unrouted_packet(0x0C010203, low)); want.append(0)      # miss: nh 0 -> FORWARD
+        frames.append(unrouted_packet(0x0A010203, 0x0A01, 0x86DD)); want.append(0)
+        frames.append(unrouted_packet(0x0B010203, 0x0A01, 0x86DD)); want.append(-1)
+        pk = np.concatenate(frames)
+        n = len(want)
+        mb = Mbufs(pk, n)
+        got = [L.process_packet(ctypes.c_void_p(mb.ptr(i))) for i in range(n)]
+        assert got == want
+        fwo, _ = oracle_tables(rules)
+        ro, _, _ = orc.process(pk, n, stages=DROPIN, fw=fwo)
+        assert list(np.where(ro["verdict"] == 0, 0, -1)) == want
+    finally:
+        assert L.coprocessor_teardown() == 0
+
+
+def _inject(ctx, what, count):
+    fn = cg.lib().cop_debug_inject
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32]
+    assert fn(ctx, what, count) == 0
+
+
+@pytest.mark.parametrize("where", ["max_pkts", "submit", "async_submit", "async_wait"])
+def test_dropin_error_paths_free_every_mbuf(rules_file, where):
+    """A failure after packets left rx_q never strands them: each dequeued
+    mbuf is forwarded or freed exactly once (switch.c:464-470 does one or the
+    other for every packet). An oversized max_pkts is refused before any
+    dequeue. Failures are injected with the library's test hook."""
+    path, rules = rules_file
+    L = cg.lib()
+    L.cop_set_mbuf_layout(0, 16)
+    L.cop_set_rule_file(path.encode())
+    assert L.coprocessor_setup() == 0
+    try:
+        ctx = L.coprocessor_ctx()
+        n = 4096
+        pk = cg.gen_trace(0x5EED0620, n, rules)
+        mb = Mbufs(pk, n)
+        fwo, _ = oracle_tables(rules)
+        _, fo, _ = orc.process(pk, n, stages=DROPIN, fw=fwo)
+        rx = L.cop_ring_create(16384)
+        tx = L.cop_ring_create(16384)
+        freed = []
+        FREE = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)
+        cb = FREE(lambda m, arg: freed.append(mb.index(m)))
+        arr = (ctypes.c_void_p * n)(*[mb.ptr(j) for j in range(n)])
+        assert L.cop_ring_enqueue_bulk(rx, arr, n, None) == n
+        stats = cg.NfStats()
+        if where == "max_pkts":
+            assert L.cop_coprocessor_poll(ctx, rx, tx, 262145, cb, None, ctypes.byref(stats)) < 0
+            assert L.cop_coprocessor_poll_async(ctx, rx, tx, 1 << 20, cb, None, ctypes.byref(stats)) < 0
+            assert L.cop_ring_count(rx) == n and not freed     # nothing was dequeued
+            return
+        if where == "submit":
+            _inject(ctx, 1, 1)
+            assert L.cop_coprocessor_poll(ctx, rx, tx, 1000, cb, None, ctypes.byref(stats)) < 0
+            lost = list(range(1000))
+        elif where == "async_submit":
+            _inject(ctx, 1, 1)
+            assert L.cop_coprocessor_poll_async(ctx, rx, tx, 1000, cb, None, ctypes.byref(stats)) < 0
+            lost = list(range(1000))
+        else:
+            assert L.cop_coprocessor_poll_async(ctx, rx, tx, 1000, cb, None, ctypes.byref(stats)) == 0
+            _inject(ctx, 2, 1)
+            # the second call submits packets 1000..1999, then completes the
+            # first batch, whose wait fails: packets 0..999 are freed
+            assert L.cop_coprocessor_poll_async(ctx, rx, tx, 1000, cb, None, ctypes.byref(stats)) < 0
+            lost = list(range(1000))
+        assert sorted(freed) == lost
+        assert stats.tx_dropped == len(lost) and stats.tx_packets == 0
+        # the loop recovers: the rest flows normally
+        del freed[:]
+        done = 0
+        while True:
+            r = L.cop_coprocessor_poll_async(ctx, rx, tx, 1000, cb, None, ctypes.byref(stats))
+            assert r >= 0
+            done += r
+            if r == 0 and L.cop_ring_count(rx) == 0:
+                break
+        assert L.cop_coprocessor_flush(ctx, tx, cb, None, ctypes.byref(stats)) >= 0
+        out = []
+        buf = (ctypes.c_void_p * 256)()
+        while True:
+            k = L.cop_ring_dequeue_burst(tx, buf, 256, None)
+            if not k:
+                break
+            out += [mb.index(buf[i]) for i in range(k)]
+        rest = set(range(1000, n))
+        assert out == [i for i in fo if i in rest]
+        assert sorted(freed) == sorted(rest - set(out))
         L.cop_ring_free(rx)
         L.cop_ring_free(tx)
     finally:

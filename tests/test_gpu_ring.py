@@ -1,13 +1,10 @@
-"""GPU parity at bench-scale launch shapes for both kernels: the one-shot
-kernel (csrc/cop_kernels.hip: coalesced loads, batches interleaved over
-workgroups, LDS-staged forward lists) and the persistent batch-sweep kernel
-(csrc/cop_stream.hip), plus the hand-offs between the two on one launch lane.
-
-Every other GPU test also runs with the batch-sweep kernel forced
-(conftest.kernel_mode), so these add the large-launch shapes: batch rings of
-64k-packet slots (the bench's layout), DIR-24-8 stages, demux and port
-statistics, rule counters, and non-uniform descriptor batches. Bit-exact
-against the oracle on every record and every forward list.
+"""GPU parity at bench-scale launch shapes (csrc/cop_kernels.hip: coalesced
+loads, batches interleaved over workgroups, LDS-staged forward lists):
+batch rings of 64k-packet slots (the bench's layout), DIR-24-8 stages, demux
+and port statistics, rule counters, non-uniform descriptor batches, and the
+runtime's state hand-offs between launches on one lane (ticket buffers,
+look-back growth, counter resets). Bit-exact against the oracle on every
+record and every forward list.
 """
 import numpy as np
 import pytest
@@ -86,7 +83,6 @@ def test_auto_ring_fw1k_bench_shape(gpu_ctx_factory):
     (2.6M packets), wrapping; the kernel the library picks by itself."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F)
-    ctx.set_kernel_mode(cg.KERNEL_AUTO)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     B, P = 65536, 40
     pk = cg.gen_trace(0x5EED0A00, B * P, rules)
@@ -99,7 +95,7 @@ def test_auto_ring_fw1k_bench_shape(gpu_ctx_factory):
 
 
 @pytest.mark.parametrize("fw_dir", [False, True])
-def test_stream_fw_lpm_dir24(gpu_ctx_factory, fw_dir):
+def test_ring_fw_lpm_dir24(gpu_ctx_factory, fw_dir):
     """FW + route LPM 100k (DIR-24-8 in HBM: the late-prefetch variant),
     firewall either in LDS or forced to DIR-24-8 too."""
     rules = fw1k()
@@ -116,11 +112,10 @@ def test_stream_fw_lpm_dir24(gpu_ctx_factory, fw_dir):
     check_slots(res, fwd, cnt, ro, fos, B, range(P))
 
 
-def test_stream_mbuf_layout_ring(gpu_ctx_factory):
-    """Slots at mbuf stride (2176 B) with 128 B headroom, streaming kernel."""
+def test_ring_mbuf_layout(gpu_ctx_factory):
+    """Slots at mbuf stride (2176 B) with 128 B headroom."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F)
-    ctx.set_kernel_mode(cg.KERNEL_STREAM)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     B, P = 30000 + 5, 5
     pk = cg.gen_trace(0x5EED0A20, B * P, rules)
@@ -130,12 +125,11 @@ def test_stream_mbuf_layout_ring(gpu_ctx_factory):
     check_slots(res, fwd, cnt, ro, fos, B, range(P))
 
 
-def test_stream_descriptor_ragged_batches(gpu_ctx_factory):
+def test_descriptor_ragged_batches(gpu_ctx_factory):
     """Descriptor submit with non-uniform batches (0, 1, 255, 1025, 70000,
-    and large ones): the tile -> batch scan of the streaming kernel."""
+    and large ones): the tile -> batch scan."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F)
-    ctx.set_kernel_mode(cg.KERNEL_STREAM)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     sizes = [0, 1, 255, 1025, 70000, 262144, 3, 200000, 0, 131072]
     n = sum(sizes)
@@ -166,12 +160,10 @@ def test_stream_descriptor_ragged_batches(gpu_ctx_factory):
         lo += m
 
 
-def test_stream_demux_port_stats(gpu_ctx_factory):
-    """Per-port ordered forward lists and per-port counters under the
-    streaming kernel at bench scale."""
+def test_ring_demux_port_stats(gpu_ctx_factory):
+    """Per-port ordered forward lists and per-port counters at bench scale."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_DEMUX_PORTS | cg.CFG_PORT_STATS)
-    ctx.set_kernel_mode(cg.KERNEL_AUTO)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     B, P, K = 65536, 36, 5
     pk = cg.gen_trace(0x5EED0A40, B * P, rules)
@@ -192,46 +184,50 @@ def test_stream_demux_port_stats(gpu_ctx_factory):
         assert ps[q]["tx_packets"] == int(np.sum((ro["port"] == q) & (ro["verdict"] == 0)))
 
 
-def test_kernel_handoffs_on_one_lane(gpu_ctx_factory):
-    """One-shot and streaming launches alternating on the same lane (the
-    ticket buffers' double-buffer protocol and look-back epochs carry
-    across both kernels)."""
+@pytest.mark.parametrize("ppt", ["1", "4", "8"])
+def test_lane_state_handoffs(gpu_ctx_factory, monkeypatch, ppt):
+    """Launches of growing size on ONE lane: every tile size ($COP_PPT) and
+    launches long enough to outgrow the lane's look-back words (the growth
+    path re-zeroes them in stream order before the kernel that uses them),
+    the ticket buffers' double-buffer protocol across launches, and a
+    counter reset between launches (it completes before the next kernel).
+    The 64-slot launch at PPT 1 (16384 tiles) once hit a look-back timeout
+    when the growth used an unordered null-stream memset."""
+    monkeypatch.setenv("COP_PPT", ppt)
     rules = fw1k()
-    ctx = gpu_ctx_factory(stages=S | F, n_streams=1)
+    ctx = gpu_ctx_factory(stages=S | F, n_streams=1, max_batch=65536, max_batches=4)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
-    B, P = 65536, 6
+    B, P = 65536, 8
     pk = cg.gen_trace(0x5EED0A50, B * P, rules)
     fw, _ = oracle_tables(rules)
     ro, fos = oracle_slots(pk, B, P, S | F, fw)
-    slot_bytes = B * 64
-    dp = ctx.alloc(slot_bytes * P)
+    dp = ctx.alloc(B * 64 * P)
     dp.upload(pk)
     dr = ctx.alloc(B * P * 8)
     df = ctx.alloc(B * P * 4)
     dc = ctx.alloc(P * 4)
-    ring = cg.make_ring(dp, P, B, dr, slot_bytes, stride=64, fwd_idx=df, fwd_slot=B, fwd_count=dc)
-    modes = [cg.KERNEL_ONESHOT, cg.KERNEL_STREAM, cg.KERNEL_STREAM, cg.KERNEL_ONESHOT, cg.KERNEL_ONESHOT,
-             cg.KERNEL_STREAM, cg.KERNEL_ONESHOT]
-    for i, m in enumerate(modes * 3):
-        ctx.set_kernel_mode(m)
-        ctx.submit_ring(ring, i % P, P)
-        if i % 4 == 3:
+    ring = cg.make_ring(dp, P, B, dr, B * 64, stride=64, fwd_idx=df, fwd_slot=B, fwd_count=dc)
+    total = 0
+    for i, count in enumerate((1, 4, 20, 64, 3, 64, 128)):
+        ctx.submit_ring(ring, i % P, count)
+        total += count
+        if i == 2:
             ctx.sync()
+            assert ctx.counters(reset=True)["rx"] == total * B
+            total = 0
     ctx.sync()
     res = dr.download(cg.RESULT_DT, B * P)
     fwd = df.download(np.uint32, B * P)
     cnt = dc.download(np.uint32, P)
     check_slots(res, fwd, cnt, ro, fos, B, range(P))
-    c = ctx.counters()
-    assert c["rx"] == B * P * len(modes) * 3
+    assert ctx.counters()["rx"] == total * B
 
 
-def test_stream_rule_counters(gpu_ctx_factory):
-    """Per-rule hit counters under the streaming kernel equal the oracle's
-    per-rule hits summed over the launch."""
+def test_ring_rule_counters(gpu_ctx_factory):
+    """Per-rule hit counters at bench scale equal the oracle's per-rule hits
+    summed over the launch."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_RULE_COUNTERS)
-    ctx.set_kernel_mode(cg.KERNEL_STREAM)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     B, P = 65536, 8
     pk = cg.gen_trace(0x5EED0A60, B * P, rules)

@@ -79,6 +79,12 @@ def run(stages, Lb, compact, label, ring=False):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "short":
+        # the driver's short timed region: one ring launch of 20 batches; one batch
+        run(S | F, 20, True, "fw ring L20 compact", ring=True)
+        run(S | F, 1, True, "fw ring L1 compact", ring=True)
+        run(S | F, 1, False, "fw ring L1 no-compact", ring=True)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "ring":
         run(S | F, 96, True, "fw ring L96 compact", ring=True)
         run(S | F | L, 96, True, "fw+lpm ring L96 compact", ring=True)
