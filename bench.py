@@ -136,6 +136,9 @@ def main():
                     help="batches per kernel launch (ring submit, at most 1024; 0: the workload's default). The "
                          "~23 us per-launch ramp and tail cost 6 %% at 384 batches, 2.5 %% at 1024")
     ap.add_argument("--streams", type=int, default=1, help="launch lanes (concurrent streams)")
+    ap.add_argument("--engine", default="pmd", choices=("pmd", "launch"),
+                    help="pmd: the poll-mode kernel serves the batch ring (steps are posted to it); launch: one "
+                         "kernel launch per --per-launch steps")
     ap.add_argument("--pool-mib", type=int, default=0,
                     help="distinct input bytes per GPU (0: max(400 MiB, one launch of batches))")
     ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the value is their median")
@@ -221,30 +224,65 @@ def main():
     else:
         ring = cg.make_ring(d_pkts, P, B, d_res, per_batch, stride=64, fwd_idx=d_fwd, fwd_count=d_cnt)
 
+    pmd = None
+
+    def pmd_on():
+        nonlocal pmd
+        if args.engine == "pmd" and pmd is None:
+            pmd = ctx.pmd_start(ring)
+
+    def pmd_off():
+        nonlocal pmd
+        if pmd is not None:
+            pmd.stop()
+            pmd = None
+
     def run_steps(first, count):
+        """Steps first .. first+count-1: batch s sits in ring slot s % P."""
+        if pmd is not None:
+            # the poll-mode kernel's batch sequence is the step sequence;
+            # posts of at most a quarter of the ring keep it from draining
+            # (a post waits only for the slots it reuses)
+            s = 0
+            while s < count:
+                k = min(max(1, P // 4), count - s)
+                pmd.post(k)
+                s += k
+            return
         s = first
         while s < first + count:
             k = min(Lb, first + count - s)
             ctx.submit_ring(ring, s % P, k)
             s += k
 
+    def sync_all():
+        if pmd is not None:
+            pmd.wait()
+        ctx.sync()
+
     # ---- warmup, then exactly K timed steps, `repeats` times; the value is
     # the median run (SURVEY.md §8d: median of 5 runs) ----
+    pmd_on()
     run_steps(0, args.warmup)
     runs, own_runs = [], []
     red_tot = None
     for r in range(max(1, args.repeats)):
-        ctx.sync()
+        pmd_on()
+        sync_all()
         group.barrier()
-        ctx.sync()
+        sync_all()
         t0 = time.perf_counter()
         run_steps(args.warmup + r * args.steps, args.steps)
         if rc_on:
-            # one reporting interval: sum counters + per-rule hits over all GPUs
+            # one reporting interval: sum counters + per-rule hits over all
+            # GPUs (the RCCL kernels need the CUs the poll-mode kernel holds:
+            # it completes and stops first, inside the timing)
+            sync_all()
+            pmd_off()
             tot, _ = ctx.coll_reduce_counters(reset=True, with_rules=False)
             if red_tot is None:
                 red_tot = tot   # the first interval also holds the warmup
-        ctx.sync()
+        sync_all()
         t1 = time.perf_counter()
         group.barrier()
         own_runs.append(t1 - t0)
@@ -255,8 +293,35 @@ def main():
     # this rank's own rate (its own clock, not the max over ranks), and its device
     own_rate = args.steps * B / float(np.median(own_runs)) / 1e6
     ranks_info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(own_rate, 3)})
-    log(f"[rank {rank}] timed {args.steps} steps x {len(runs)} runs, median {elapsed * 1e3:.2f} ms "
+    log(f"[rank {rank}] timed {args.steps} steps x {len(runs)} runs ({args.engine}), median {elapsed * 1e3:.3f} ms "
         f"-> {value:.1f} Mpkt/s (all ranks); runs {[round(x * 1e3, 3) for x in runs]} ms")
+
+    # ---- the poll-mode kernel's steady state and single-batch latency ----
+    pmd_info = None
+    if args.engine == "pmd":
+        pmd_on()
+        sync_all()
+        n_long = min(P, 1024)
+        longs = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            pmd.post(n_long)
+            pmd.wait()
+            longs.append(time.perf_counter() - t0)
+        lat = []
+        for _ in range(50):
+            t0 = time.perf_counter()
+            pmd.post(1)
+            pmd.wait()
+            lat.append((time.perf_counter() - t0) * 1e6)
+        info = pmd.info()
+        t_long = float(np.median(longs))
+        pmd_info = {"workers": info["workers"], "workers_per_cu": info["workers_per_cu"],
+                    "packets_per_tile": info["packets_per_tile"], "launches": info["launches"],
+                    "steady_batches": n_long, "steady_mpkt_s": round(n_long * B / t_long / 1e6, 3),
+                    "steady_ms": round(t_long * 1e3, 4),
+                    "single_batch_post_to_done_us_median": round(float(np.median(lat)), 2)}
+        pmd_off()
 
     reduce_info = None
     if rc_on:
@@ -272,6 +337,8 @@ def main():
         log(f"[rank {rank}] rccl counter all-reduce of {1024 + n_rules} u64: {r_ms:.3f} ms")
 
     # ---- kernel duration per launch (HIP events on the context stream) ----
+    run_steps(0, Lb)   # untimed: loads the one-shot kernel's code object (first launch)
+    ctx.sync()
     ctx.counters(reset=True)
     ctx.launch_timing(True)
     nl = max(8, min(200, args.steps // Lb))
@@ -348,6 +415,7 @@ def main():
             "parallelism": f"independent per-GPU contexts x{world} (no data-path collective)",
             "pool_batches": int(P),
             "rule_counters": rc_on,
+            "engine": args.engine,
             "ranks": ranks_info,
         },
         "roofline": {
@@ -379,6 +447,11 @@ def main():
         "cpu_baseline": None,
     }
     out["single_batch_latency"] = single_batch
+    if pmd_info:
+        # the poll-mode kernel: a 1024-batch post (HBM-resident, one post, no
+        # launch) timed on the host, as a fraction of the peak
+        pmd_info["steady_frac"] = round(pmd_info["steady_mpkt_s"] * 1e6 * bytes_per_pkt / 1e9 / HBM_PEAK_GBS, 4)
+        out["pmd"] = pmd_info
     if reduce_info:
         out["counter_reduce"] = reduce_info
 

@@ -80,6 +80,12 @@ class TraceOpts(Structure):
                 ("pct_src_in_rule", c_uint32)]
 
 
+class PmdInfo(Structure):
+    _fields_ = [("workers", c_uint32), ("workers_per_cu", c_uint32), ("tiles_per_batch", c_uint32),
+                ("packets_per_tile", c_uint32), ("launches", c_uint32), ("state", c_uint32),
+                ("posted", c_uint64), ("completed", c_uint64)]
+
+
 class NfStats(Structure):
     _fields_ = [("rx_packets", c_uint64), ("rx_dropped", c_uint64), ("tx_packets", c_uint64),
                 ("tx_dropped", c_uint64)]
@@ -119,6 +125,12 @@ SIGNATURES = {
     "cop_submit": (c_int, [c_void_p, POINTER(Batch), c_uint32]),
     "cop_submit_ring": (c_int, [c_void_p, POINTER(BatchRing), c_uint32, c_uint32]),
     "cop_sync": (c_int, [c_void_p]),
+    "cop_pmd_start": (c_int, [c_void_p, POINTER(BatchRing), POINTER(c_void_p)]),
+    "cop_pmd_post": (c_int, [c_void_p, c_uint32]),
+    "cop_pmd_wait": (c_int, [c_void_p, c_uint64]),
+    "cop_pmd_posted": (c_uint64, [c_void_p]),
+    "cop_pmd_info": (c_int, [c_void_p, POINTER(PmdInfo)]),
+    "cop_pmd_stop": (c_int, [c_void_p]),
     "cop_poll": (c_int, [c_void_p]),
     "cop_process_host": (c_int, [c_void_p, POINTER(c_void_p), c_uint32, c_void_p, c_void_p, c_void_p]),
     "cop_process_host_stream": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
@@ -429,6 +441,8 @@ class Context:
 
     def close(self):
         if self.handle and self.handle.value:
+            for m in getattr(self, "_pmds", []):
+                m.stop()
             lib().cop_destroy(self.handle)
             self.handle = c_void_p()
 
@@ -464,6 +478,10 @@ class Context:
 
     def alloc(self, nbytes) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
+
+    def pmd_start(self, ring: "BatchRing") -> "Pmd":
+        """Start the poll-mode (persistent) kernel serving `ring`."""
+        return Pmd(self, ring)
 
     def submit(self, batches):
         arr = (Batch * len(batches))(*batches)
@@ -558,6 +576,52 @@ class Context:
         _check(lib().cop_launch_timing_read(self.handle, byref(ms), byref(n), 1 if reset else 0), self,
                "launch_timing_read")
         return ms.value, n.value
+
+
+class Pmd:
+    """A poll-mode kernel serving one batch ring (cop_pmd_*): post(count)
+    hands the next `count` slots to the running kernel (batch sequence
+    numbers continue across posts; batch b sits in slot b % n_slots),
+    wait(seq) blocks until batches < seq have completed."""
+
+    def __init__(self, ctx: "Context", ring: "BatchRing"):
+        self.ctx = ctx
+        self.ring = ring   # keep the descriptor alive
+        self.handle = c_void_p()
+        _check(lib().cop_pmd_start(ctx.handle, byref(ring), byref(self.handle)), ctx, "pmd_start")
+        if not hasattr(ctx, "_pmds"):
+            ctx._pmds = []
+        ctx._pmds.append(self)
+
+    def post(self, count: int):
+        _check(lib().cop_pmd_post(self.handle, count), self.ctx, "pmd_post")
+
+    def wait(self, seq: int | None = None):
+        if seq is None:
+            seq = self.posted
+        _check(lib().cop_pmd_wait(self.handle, seq), self.ctx, "pmd_wait")
+
+    @property
+    def posted(self) -> int:
+        return int(lib().cop_pmd_posted(self.handle))
+
+    def info(self) -> dict:
+        i = PmdInfo()
+        _check(lib().cop_pmd_info(self.handle, byref(i)), self.ctx, "pmd_info")
+        return {k: getattr(i, k) for k, _ in PmdInfo._fields_}
+
+    def stop(self):
+        if self.handle and self.handle.value:
+            h, self.handle = self.handle, c_void_p()
+            if self in getattr(self.ctx, "_pmds", []):
+                self.ctx._pmds.remove(self)
+            _check(lib().cop_pmd_stop(h), self.ctx, "pmd_stop")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.stop()
 
 
 def make_ring(pkts, n_slots: int, n: int, results, pkts_slot_bytes: int, results_slot: int = 0,

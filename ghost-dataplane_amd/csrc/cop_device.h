@@ -40,6 +40,41 @@ __device__ __forceinline__ unsigned long long lb_load(unsigned long long *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Output stores. The one-shot kernel stores non-temporally (the lines sit
+// in the XCD's L2 until the kernel-end write-back); the poll-mode kernel
+// has no kernel end per batch, so WT (write-through, sc1) stores make a
+// batch's records and forward list visible to the host and to every XCD
+// once the storing waves have drained (vmcnt(0)) and the batch is
+// signalled (MI355X_MICROARCH.md, Valid forms: sc1 stores + drain + flag).
+template <bool WT>
+__device__ __forceinline__ void st_u32x2(u32x2 v, u32x2 *p)
+{
+    if (WT)
+        __hip_atomic_store((unsigned long long *)p, ((unsigned long long)v.y << 32) | v.x, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    else
+        __builtin_nontemporal_store(v, p);
+}
+
+template <bool WT>
+__device__ __forceinline__ void st_u32(uint32_t v, uint32_t *p)
+{
+    if (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __builtin_nontemporal_store(v, p);
+}
+
+// 16 bytes at list word w of `base`: a buffer store with sc1 (aux 16) when WT
+template <bool WT>
+__device__ __forceinline__ void st_u32x4(u32x4 v, uint32_t *base, long w)
+{
+    if (WT) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(w * 4), 0, 16);
+    } else {
+        __builtin_nontemporal_store(v, (u32x4 *)(base + w));
+    }
+}
+
 // Workgroup barrier that orders LDS only. __syncthreads() is a workgroup
 // fence plus s_barrier, and the fence waits for every outstanding global load
 // and store of the wave (vmcnt(0)): prefetched tiles and in-flight record
@@ -321,9 +356,9 @@ __device__ __forceinline__ Opt opt_all(const CopKParams &p)
 
 // LDS views of the tables (staged at workgroup start)
 struct Tables {
-    const uint32_t *rt_top;
-    const uint16_t *rt_leaf;
-    const uint32_t *fw_s, *fw_v, *lp_s, *lp_v;
+    uint32_t *rt_top;
+    uint16_t *rt_leaf;
+    uint32_t *fw_s, *fw_v, *lp_s, *lp_v;
 };
 
 // Pass 1, per step: parse, vport route (stage P), interval searches in LDS,
@@ -441,7 +476,7 @@ struct Counts {
     uint32_t total = 0, notv4 = 0, fwd = 0, dropfw = 0, parse = 0, noport = 0, rhit = 0, rx = 0;
 };
 
-template <int PPT>
+template <int PPT, bool WT>
 __device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base, int tid, const bool (&valid)[PPT],
                                               const uint32_t (&verdict)[PPT], const uint32_t (&flags)[PPT],
                                               const uint32_t (&port)[PPT], const uint32_t (&rnh)[PPT],
@@ -454,7 +489,7 @@ __device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base,
             u32x2 rec;
             rec.x = verdict[k] | (flags[k] << 8) | (port[k] << 16);
             rec.y = rnh[k];
-            __builtin_nontemporal_store(rec, &((u32x2 *)B.results)[base + k * BLOCK + tid]);
+            st_u32x2<WT>(rec, &((u32x2 *)B.results)[base + k * BLOCK + tid]);
             c.rx++;
             c.fwd += verdict[k] == COPK_FORWARD;
             c.dropfw += verdict[k] == COPK_DROP_FW;
@@ -468,6 +503,7 @@ __device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base,
 // Copy a tile's forward list (agg indices staged in LDS, in order) to
 // fwd_idx[pref ..]: 16-byte non-temporal stores on 16-byte boundaries of
 // the list, partial words only at the two ends. All BLOCK data threads.
+template <bool WT>
 __device__ __forceinline__ void copy_out_list(uint32_t *fwd_idx, uint32_t pref, uint32_t agg, const uint32_t *stage,
                                               int tid)
 {
@@ -484,16 +520,24 @@ __device__ __forceinline__ void copy_out_list(uint32_t *fwd_idx, uint32_t pref, 
             v.y = stage[i + 1];
             v.z = stage[i + 2];
             v.w = stage[i + 3];
-            __builtin_nontemporal_store(v, (u32x4 *)&fwd_idx[w0]);
+            st_u32x4<WT>(v, fwd_idx, w0);
         } else {
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const long w = w0 + i;
-                if (w >= (long)pref && w < end) __builtin_nontemporal_store(stage[w - (long)pref], &fwd_idx[w]);
+                if (w >= (long)pref && w < end) st_u32<WT>(stage[w - (long)pref], &fwd_idx[w]);
             }
         }
     }
 }
+
+// The look-back chain state of a launch (one-shot kernel) or of one batch
+// (poll-mode kernel: epoch = the batch's sequence tag).
+struct LookCtx {
+    unsigned long long *look;
+    uint32_t epoch;
+    uint32_t *err;
+};
 
 // LDS scratch of one compaction: per-(step, wave) counts and the prefix of
 // the single-list form, or per-port counts and prefixes with demux.
@@ -515,8 +559,8 @@ struct CompactLds {
 // mid() runs between the look-back and the second barrier: the caller's
 // record stores go there, so the look-back's loads (vmcnt retires in order)
 // do not wait for them and the other waves store while wave 0 looks back.
-template <int PPT, typename Mid>
-__device__ __forceinline__ void compact_tile(const CopKParams &p, const Opt &o, const CopKBatch &B, uint32_t lb_off,
+template <int PPT, bool WT, typename Mid>
+__device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, const CopKBatch &B, uint32_t lb_off,
                                              uint32_t j,
                                              uint32_t base, const bool (&fwd)[PPT], const uint32_t (&port)[PPT],
                                              const CompactLds &s, int tid, int lane, int wave, Mid mid)
@@ -549,24 +593,24 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const Opt &o, 
         if (wave == 0) {
             // dbg bit 32 (timing-only ablation): no look-back wait, wrong offsets
             const uint32_t excl =
-                (o.dbg & 32u) ? j * 1024u : look_back(p.look + lb_off, 1u, j, agg, p.epoch, p.err, lane);
+                (o.dbg & 32u) ? j * 1024u : look_back(lk.look + lb_off, 1u, j, agg, lk.epoch, lk.err, lane);
             if (lane == 0) {
                 *s.pref = excl;
-                if (B.fwd_count && j == B.ntiles - 1) *B.fwd_count = excl + agg;
+                if (B.fwd_count && j == B.ntiles - 1) st_u32<WT>(excl + agg, B.fwd_count);
             }
         }
         mid();
         lds_barrier();
         const uint32_t pref = *s.pref;
         if (staged) {
-            copy_out_list(B.fwd_idx, pref, agg, s.stage, tid);
+            copy_out_list<WT>(B.fwd_idx, pref, agg, s.stage, tid);
         } else if (B.fwd_idx && !(o.dbg & 64u)) {
 #pragma unroll
             for (int k = 0; k < PPT; k++) {
                 if (fwd[k]) {
                     const uint32_t r = __builtin_amdgcn_mbcnt_hi(
                         (uint32_t)(bal[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u));
-                    __builtin_nontemporal_store(base + k * BLOCK + tid, &B.fwd_idx[pref + off[k] + r]);
+                    st_u32<WT>(base + k * BLOCK + tid, &B.fwd_idx[pref + off[k] + r]);
                 }
             }
         }
@@ -585,10 +629,10 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const Opt &o, 
         uint32_t agg;
         const uint32_t ex = wave_excl_scan(lane < NQ ? s.dq[q * NQ + lane] : 0u, NQ, lane, &agg);
         if (lane < NQ) s.dq[q * NQ + lane] = ex;
-        const uint32_t excl = look_back(p.look + (size_t)lb_off * K + q, K, j, agg, p.epoch, p.err, lane);
+        const uint32_t excl = look_back(lk.look + (size_t)lb_off * K + q, K, j, agg, lk.epoch, lk.err, lane);
         if (lane == 0) {
             s.dpref[q] = excl;
-            if (B.fwd_count && j == B.ntiles - 1) B.fwd_count[q] = excl + agg;
+            if (B.fwd_count && j == B.ntiles - 1) st_u32<WT>(excl + agg, &B.fwd_count[q]);
         }
     }
     mid();
@@ -605,8 +649,8 @@ __device__ __forceinline__ void compact_tile(const CopKParams &p, const Opt &o, 
             }
             if (fwd[k]) {
                 const uint32_t q = port[k];
-                __builtin_nontemporal_store(
-                    base + k * BLOCK + tid, &B.fwd_idx[(size_t)q * B.n + s.dpref[q] + s.dq[q * NQ + k * WAVES + wave] + r]);
+                st_u32<WT>(base + k * BLOCK + tid,
+                           &B.fwd_idx[(size_t)q * B.n + s.dpref[q] + s.dq[q * NQ + k * WAVES + wave] + r]);
             }
         }
     }

@@ -102,9 +102,37 @@ struct CopKParams {
     unsigned long long *stamps;   // diagnostic phase stamps (dbg bit 8)
 };
 
+// Poll-mode (persistent) kernel, cop_pmd.hip: n_work worker workgroups
+// serve a batch ring; every relay_stride-th one relays the host's doorbell.
+struct CopKPmd {
+    CopKParams k;                        // ring mode (k.rg, rg.first = 0), tables, counters,
+                                         // options; k.uniform_ntiles = tiles per batch
+    const unsigned long long *h_posted;  // host-mapped: batches posted (monotonic)
+    const uint32_t *h_stop;              // host-mapped: non-zero = leave once idle
+    unsigned long long *h_done;          // host-mapped: [slot] = sequence + 1 of its last completed batch
+    uint32_t *h_state;                   // host-mapped: [0] exit reason (COPK_PMD_*), [1] census
+    unsigned long long *d_posted;        // device relay of *h_posted
+    uint32_t *d_ctl;                     // device: [0] exit (COPK_PMD_*), [1] census, [2] look-back timeout
+    unsigned long long *slot_tiles;      // per ring slot: tiles completed (monotonic)
+    unsigned long long *stamps;          // diagnostic: s_memrealtime per worker phase (COP_PMD_STAMPS) or null
+    unsigned long long seq0;             // first batch sequence this launch serves
+    uint32_t n_work;                     // worker workgroups
+    uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
+    uint32_t idle_ticks;                 // s_memrealtime ticks (100 MHz) without a post before leaving
+};
+#define COPK_PMD_RUNNING 0u
+#define COPK_PMD_STOPPED 1u   /* the host asked (cop_pmd_stop) */
+#define COPK_PMD_IDLE 2u      /* no post for idle_ticks: left; the next post relaunches */
+#define COPK_PMD_ABORT 3u     /* not every worker became resident, or a look-back timed out */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
+hipError_t copk_pmd_launch(const CopKPmd *p, int fw_mode, int lpm_mode, int layout, int ppt, int ext,
+                           uint32_t lds_bytes, hipStream_t stream);
+// resident workgroups per CU of that kernel at lds_bytes (the occupancy API)
+hipError_t copk_pmd_occupancy(int fw_mode, int lpm_mode, int layout, int ppt, int ext, uint32_t lds_bytes,
+                              int *per_cu);
 // layout: COPK_LAY_*
 hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int layout, int ppt,
                        uint32_t grid, uint32_t lds_bytes, hipStream_t stream);

@@ -31,21 +31,11 @@
 
 #include "cop_device.h"
 #include "cop_kernels.h"
+#include "cop_tile.h"
 
 namespace {
 
 using namespace copd;
-
-// diagnostic-only phase stamps (p.dbg bit 8): wave 0 lane 0 writes
-// s_memrealtime (100 MHz) per phase into a buffer nothing else reads
-#define STAMP(ph)                                                                          \
-    do {                                                                                   \
-        if ((o.dbg & 8u) && tid == 0) {                                                    \
-            __builtin_amdgcn_sched_barrier(0);                                             \
-            p.stamps[blockIdx.x * 8 + (ph)] = __builtin_amdgcn_s_memrealtime();            \
-            __builtin_amdgcn_sched_barrier(0);                                             \
-        }                                                                                  \
-    } while (0)
 
 // experiment builds may raise the occupancy target (KDEFS=-DCOPK_WAVES_PER_EU=8)
 #ifndef COPK_WAVES_PER_EU
@@ -61,38 +51,12 @@ using namespace copd;
 template <int FW, int LPM, int LAY, int PPT, bool EXT>
 __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const CopKParams p)
 {
-    constexpr bool IMIX = LAY == COPK_LAY_IMIX;
     const Opt o = EXT ? opt_all(p) : Opt{0u, 0u, 0u, nullptr};
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    constexpr int TILE = BLOCK * PPT;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-
-    // ---- LDS carve (offsets in u32 words, all multiples of 4) ----
-    Tables tb;
-    uint32_t *rt_top = lds;                                  // 256
-    uint16_t *rt_leaf = (uint16_t *)(lds + 256);             // nleaf*256 u16
-    uint32_t *fw_s = lds + p.lds_fw_off;
-    uint32_t *fw_v = fw_s + p.fw_m;
-    uint32_t *lp_s = lds + p.lds_lpm_off;
-    uint32_t *lp_v = lp_s + p.lpm_m;
-    tb.rt_top = rt_top;
-    tb.rt_leaf = rt_leaf;
-    tb.fw_s = fw_s;
-    tb.fw_v = fw_v;
-    tb.lp_s = lp_s;
-    tb.lp_v = lp_v;
-    uint32_t *misc = lds + p.lds_misc_off;
-    uint32_t *s_tile = misc + 32;
-    uint32_t *s_red = misc + 40;                              // [WAVES][8]
-    CompactLds cl;
-    cl.cnt = misc;                                            // [PPT*WAVES]
-    cl.pref = misc + 33;
-    cl.dq = misc + COPK_LDS_MISC_WORDS;                       // [K][PPT*WAVES]
-    cl.dpref = cl.dq + COPK_MAX_DEMUX_PORTS * PPT * WAVES;    // [K]
-    uint32_t *s_ps = cl.dpref + 8;                   // [WAVES][16]
-    cl.stage = p.lds_stage_off ? lds + p.lds_stage_off : nullptr;   // [TILE]
+    const LdsCarve lc = lds_carve<PPT>(p, lds);
 
     STAMP(0);
     // ---- batch of this workgroup: static blockIdx ranges ----
@@ -118,114 +82,19 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
     if (dyn && tid == 0) tk = atomicAdd(&p.tickets[b * 16], 1ull);
 
     // ---- stage tables into LDS by LDS-DMA while the ticket is in flight ----
-    if (!(o.dbg & 4u)) {
-        lds_stage(rt_top, p.rt_top, 64, lane, wave);
-        lds_stage((uint32_t *)rt_leaf, p.rt_leaf, p.rt_nleaf * 32u, lane, wave);
-        if (FW == COPK_TBL_IVT) {
-            lds_stage(fw_s, p.fw_starts, p.fw_m >> 2, lane, wave);
-            lds_stage(fw_v, p.fw_vals, p.fw_m >> 2, lane, wave);
-        }
-        if (LPM == COPK_TBL_IVT) {
-            lds_stage(lp_s, p.lpm_starts, p.lpm_m >> 2, lane, wave);
-            lds_stage(lp_v, p.lpm_vals, p.lpm_m >> 2, lane, wave);
-        }
-    }
+    if (!(o.dbg & 4u)) stage_tables<FW, LPM>(p, lc.tb, lane, wave);
     uint32_t j;
     if (dyn) {
-        if (tid == 0) *s_tile = (uint32_t)tk;
+        if (tid == 0) *lc.s_tile = (uint32_t)tk;
         __syncthreads();
-        j = __builtin_amdgcn_readfirstlane(*s_tile);
+        j = __builtin_amdgcn_readfirstlane(*lc.s_tile);
     } else {
         j = ilv ? g / p.nb : p.uniform_ntiles ? g - b * p.uniform_ntiles : g - p.tile_begin[b];
     }
-    const uint32_t base = j * TILE;
     STAMP(1);
 
-    // ---- packet header loads (all PPT packets, no branches). Lanes past
-    // the end of the batch re-read the last packet and are masked out of
-    // every store and count. ----
-    uint32_t w3[PPT], w6[PPT], w7[PPT], w8[PPT];
-    bool valid[PPT];
-    const uint32_t last = B.n ? B.n - 1 : 0u;
-    if (LAY == COPK_LAY_COALESCED && B.n) {
-        const StepGeom sg = step_geom(lane);
-        u32x4 v[PPT][3];
-#pragma unroll
-        for (int k = 0; k < PPT; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
-#pragma unroll
-        for (int k = 0; k < PPT; k++) gather_step(sg, v[k], w3[k], w6[k], w7[k], w8[k]);
-    } else if (LAY == COPK_LAY_HDR16 && B.n) {
-        // one 16-byte record per packet: frame bytes 12..15 then 24..35
-#pragma unroll
-        for (int k = 0; k < PPT; k++) {
-            const uint32_t ic = min(base + k * BLOCK + tid, last);
-            const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(B.pkts + B.data_off + (size_t)ic * 16u));
-            w3[k] = v.x;
-            w6[k] = v.y;
-            w7[k] = v.z;
-            w8[k] = v.w;
-        }
-    } else if (B.n) {
-#pragma unroll
-        for (int k = 0; k < PPT; k++) {
-            const uint32_t ic = min(base + k * BLOCK + tid, last);
-            const uint8_t *pk;
-            if (IMIX) pk = B.pkts + B.offsets[ic] + B.data_off;
-            else pk = B.pkts + (size_t)ic * B.stride + B.data_off;
-            // two loads: bytes 12..27 (dwordx4 at a 4-byte-aligned address;
-            // w3 and w6) and 28..35 (w7, w8)
-            const u32x4a a = *(const u32x4a *)(pk + 12);
-            const u32x2a b = *(const u32x2a *)(pk + 28);
-            w3[k] = a.x;
-            w6[k] = a.w;
-            w7[k] = b.x;
-            w8[k] = b.y;
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < PPT; k++) w3[k] = w6[k] = w7[k] = w8[k] = 0;
-    }
-#pragma unroll
-    for (int k = 0; k < PPT; k++) valid[k] = base + k * BLOCK + tid < B.n;
-    if (!dyn) __syncthreads();   // LDS tables (the dynamic path synced above)
-
-    // ---- pass 1 (parse, route, LDS searches, tbl24 loads issued) ----
-    uint32_t verdict[PPT], port[PPT], flags[PPT], rnh[PPT], fwe[PPT], lpe[PPT], src[PPT], dst[PPT];
-    pass1<FW, LPM, PPT>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe);
-    if (o.dbg & 8u) {
-        uint32_t x = 0;
-#pragma unroll
-        for (int k = 0; k < PPT; k++) x ^= verdict[k] ^ src[k];
-        asm volatile("" ::"v"(x));
-    }
-    STAMP(2);
-
-    // ---- pass 2 (tbl8 step) and the verdicts ----
-    Counts cn;
-    pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, cn.total, cn.notv4);
-    rule_hit_atomics<FW, PPT>(o, valid, flags, fwe);
-    if (o.dbg & 8u) {
-        uint32_t x = 0;
-#pragma unroll
-        for (int k = 0; k < PPT; k++) x ^= verdict[k] ^ rnh[k];
-        asm volatile("" ::"v"(x));
-    }
-    STAMP(3);
-    // ---- ordered compaction (one list per batch, or per vport), with the
-    // result records (8 B per packet, coalesced) stored during its look-back
-    bool fwd[PPT];
-#pragma unroll
-    for (int k = 0; k < PPT; k++) fwd[k] = valid[k] && verdict[k] == COPK_FORWARD;
-    auto records = [&] { store_records<PPT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn); };
-    if (p.compact) compact_tile<PPT>(p, o, B, look_off, j, base, fwd, port, cl, tid, lane, wave, records);
-    else records();
-    STAMP(5);
-
-    // ---- counters (one flush per workgroup) ----
-    uint32_t prx[COPK_MAX_DEMUX_PORTS] = {}, ptx[COPK_MAX_DEMUX_PORTS] = {};
-    if (o.port_stats) port_counts<PPT>(o.port_stats, valid, fwd, port, prx, ptx);
-    flush_counters(p, o, cn, prx, ptx, s_red, s_ps, tid, lane, wave);
-    STAMP(6);
+    tile_body<FW, LPM, LAY, PPT, EXT, false>(p, o, lc, B, look_off, j, LookCtx{p.look, p.epoch, p.err}, tid, lane,
+                                             wave, !dyn);
 }
 
 template <int FW, int LPM, int LAY, int PPT>

@@ -1,0 +1,266 @@
+// cop_pmd.hip — the coprocessor NF pipeline as a poll-mode (persistent)
+// kernel: the GPU analogue of the reference's coprocessor lcores, which
+// spin on their rx rings forever (main_loop -> coprocessor(),
+// switch.c:529-535) instead of being started per burst.
+//
+// One launch serves a batch ring in HBM (cop_batch_ring) for as long as the
+// host posts batches to it. The host posts by bumping a counter in mapped
+// host memory (the doorbell); batch sequence b lives in ring slot
+// b % n_slots. The grid is n_work worker workgroups, all co-resident:
+//   - waiting workers poll a device copy of the doorbell; a few leaders
+//     also read the host counter over PCIe and raise the copy (wait_posted);
+//   - worker w processes the global tile sequence T = seq0*tpb + w, + n_work,
+//     ... (tile j = T % tpb of batch b = T / tpb; tpb tiles per batch). The
+//     assignment is static, so no ticket atomics: every tile a look-back
+//     waits on belongs to a lower T, held by a resident worker that reaches
+//     it first (no deadlock while all n_work workers are resident, which a
+//     start-up census checks).
+// A tile is the one-shot kernel's tile body (cop_tile.h) with write-through
+// (sc1) output stores; after it every wave drains its stores, and one lane
+// counts the tile for its slot; the slot's last tile writes the batch's
+// sequence + 1 into the host-mapped completion word. The look-back chain of
+// slot s is tagged with the batch sequence, so chains of successive batches
+// in one slot never mix. Tables are staged into LDS once per worker.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cop_device.h"
+#include "cop_kernels.h"
+#include "cop_tile.h"
+
+namespace {
+
+using namespace copd;
+
+constexpr uint32_t CENSUS_SPINS = 1u << 21;   // ~0.2 s of s_sleep(2) for every worker to become resident
+
+// diagnostic stamps: write-through, so a host copy sees them while the
+// kernel still runs (no kernel-end L2 write-back)
+__device__ __forceinline__ void st_stamp(unsigned long long *p, unsigned long long v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t ld_agent(uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Claim the exit word (first reason wins) and tell the host.
+__device__ __forceinline__ void pmd_leave(const CopKPmd &P, uint32_t why)
+{
+    if (atomicCAS(&P.d_ctl[0], 0u, why) == 0u)
+        __hip_atomic_store(&P.h_state[0], why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One lane of a worker waits until batch b is posted (returns the posted
+// count) or the kernel is to leave (returns 0). Doorbell leaders (every
+// relay_stride-th worker) also read the host's counter over PCIe and raise
+// the device copy every waiting worker polls: a handful of PCIe readers,
+// not one per worker, and no workgroup slot spent on a doorbell. Leaders
+// also turn the host's stop flag, a look-back timeout or an idle spell
+// (no new post for idle_ticks) into the exit word.
+__device__ unsigned long long wait_posted(const CopKPmd &P, unsigned long long b, bool leader)
+{
+    unsigned long long seen = 0, t_seen = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        unsigned long long hp = __hip_atomic_load(P.d_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (hp > b) return hp;
+        if (ld_agent(&P.d_ctl[0])) return 0;
+        if (leader) {
+            const unsigned long long h = __hip_atomic_load(P.h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            if (h > hp) {
+                atomicMax(P.d_posted, h);
+                if (P.stamps) {   // diagnostic: when each doorbell value was relayed
+                    st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2], h);
+                    st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2 + 1], now);
+                }
+                if (h > b) return h;
+            }
+            if (h != seen) {
+                seen = h;
+                t_seen = now;
+            }
+            if (ld_agent(&P.d_ctl[2])) pmd_leave(P, COPK_PMD_ABORT);   // a look-back timed out
+            else if (__hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) pmd_leave(P, COPK_PMD_STOPPED);
+            else if (now - t_seen > P.idle_ticks) pmd_leave(P, COPK_PMD_IDLE);
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// experiment builds only: COPK_PMD_WT=0 stores non-temporally (timing of the
+// write-through cost; results are then not guaranteed visible at completion)
+#ifndef COPK_PMD_WT
+#define COPK_PMD_WT 1
+#endif
+// Workers per CU (waves per SIMD): 4 for 2048-packet tiles (<= 128 VGPRs),
+// 5 for 1024-packet tiles (<= 96), 6 for 256-packet tiles (<= 80; the SGPR
+// limit admits no more, MI355X_MICROARCH.md Residency)
+#ifndef COPK_PMD_WAVES_PER_EU
+#define COPK_PMD_WAVES_PER_EU(ppt) ((ppt) == 8 ? 4 : (ppt) == 4 ? 5 : 6)
+#endif
+template <int FW, int LPM, int LAY, int PPT, bool EXT>
+__global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(const CopKPmd P)
+{
+    const CopKParams &p = P.k;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const Opt o = EXT ? opt_all(p) : Opt{0u, 0u, 0u, nullptr};
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const LdsCarve lc = lds_carve<PPT>(p, lds);
+    uint32_t *s_door = lc.s_misc + 36;   // [0..1] posted, [2] leave
+    stage_tables<FW, LPM>(p, lc.tb, lane, wave);
+
+    // census: every worker and the doorbell resident, or nobody works
+    if (tid == 0) {
+        atomicAdd(&P.d_ctl[1], 1u);
+        uint32_t spins = 0;
+        while (ld_agent(&P.d_ctl[1]) < P.n_work && ld_agent(&P.d_ctl[0]) == 0) {
+            if (++spins > CENSUS_SPINS) {
+                pmd_leave(P, COPK_PMD_ABORT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        s_door[2] = ld_agent(&P.d_ctl[0]) == COPK_PMD_ABORT ? 1u : 0u;
+    }
+    __syncthreads();   // also lands the LDS-DMA table staging
+    if (s_door[2]) return;
+    if (blockIdx.x == 0 && tid == 0)   // tell the host every worker is resident
+        __hip_atomic_store(&P.h_state[1], P.n_work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+
+    const uint32_t tpb = p.uniform_ntiles;
+    const uint32_t G = P.n_work;
+    const uint32_t n_slots = p.rg.n_slots;
+    // tile (b, j, slot) of T = seq0*tpb + blockIdx.x, advanced by G per step
+    unsigned long long b = P.seq0 + blockIdx.x / tpb;
+    uint32_t j = blockIdx.x % tpb;
+    uint32_t slot = (uint32_t)(b % n_slots);
+    const uint32_t qb = G / tpb, rb = G % tpb;
+    unsigned long long posted = 0;
+    const bool leader = blockIdx.x % P.relay_stride == 0;
+    unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
+    for (;;) {
+        if (stamp && tid == 0) st_stamp(&stamp[0], __builtin_amdgcn_s_memrealtime());   // diagnostic: tile start
+        if (b >= posted) {
+            // wait for batch b to be posted (one lane polls the relay)
+            if (tid == 0) {
+                const unsigned long long hp = wait_posted(P, b, leader);
+                s_door[0] = (uint32_t)hp;
+                s_door[1] = (uint32_t)(hp >> 32);
+                s_door[2] = hp == 0 ? 1u : 0u;
+            }
+            lds_barrier();
+            posted = ((unsigned long long)s_door[1] << 32) | s_door[0];
+            const uint32_t leave = s_door[2];
+            lds_barrier();   // s_door is rewritten only after every wave has read it
+            if (leave) break;
+        }
+        if (stamp && tid == 0) {
+            st_stamp(&stamp[1], __builtin_amdgcn_s_memrealtime());   // batch b posted (as seen here)
+            st_stamp(&stamp[4], b);
+        }
+        // The lane's index is made opaque each iteration, so the per-lane
+        // values the tile derives from it (load geometry, LDS addresses) are
+        // recomputed in the tile rather than hoisted out of the loop and held
+        // live across it: loop-invariant code motion cost the persistent
+        // kernel ~50 VGPRs over the one-shot kernel's tile.
+        int tid_i = tid;
+        asm volatile("" : "+v"(tid_i));
+        const int lane_i = tid_i & 63;
+        const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
+        uint32_t look_off;
+        const CopKBatch B = batch_desc(p, slot, &look_off);
+        tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(p, o, lc, B, look_off, j,
+                                                LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2]}, tid_i, lane_i,
+                                                wave_i, false);
+        // completion: every wave's stores (write-through) have landed, then
+        // one lane counts the tile; the slot's last tile signals the host
+        if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (tid == 0) {
+            const unsigned long long old = atomicAdd(&P.slot_tiles[slot], 1ull);
+            if ((old + 1) % tpb == 0)
+                __hip_atomic_store(&P.h_done[slot], b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (stamp) {
+                st_stamp(&stamp[3], __builtin_amdgcn_s_memrealtime());   // stores drained, tile counted
+                st_stamp(&stamp[5], (old + 1) % tpb == 0 ? 1ull : 0ull);
+            }
+        }
+        // next tile: T += G
+        j += rb;
+        uint32_t db = qb;
+        if (j >= tpb) {
+            j -= tpb;
+            db++;
+        }
+        b += db;
+        slot += db % n_slots;
+        if (slot >= n_slots) slot -= n_slots;
+    }
+}
+
+template <int FW, int LPM, int LAY, int PPT>
+hipError_t pmd_one(const CopKPmd *p, int ext, uint32_t lds, hipStream_t s, int *occ)
+{
+    if (occ) {
+        if (ext) return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, cop_pmd<FW, LPM, LAY, PPT, true>, BLOCK, lds);
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, cop_pmd<FW, LPM, LAY, PPT, false>, BLOCK, lds);
+    }
+    const dim3 grid(p->n_work);
+    if (ext) hipLaunchKernelGGL((cop_pmd<FW, LPM, LAY, PPT, true>), grid, dim3(BLOCK), lds, s, *p);
+    else hipLaunchKernelGGL((cop_pmd<FW, LPM, LAY, PPT, false>), grid, dim3(BLOCK), lds, s, *p);
+    return hipGetLastError();
+}
+
+template <int FW, int LPM, int LAY>
+hipError_t pmd_ppt(const CopKPmd *p, int ppt, int ext, uint32_t lds, hipStream_t s, int *occ)
+{
+    if (ppt == 8) return pmd_one<FW, LPM, LAY, 8>(p, ext, lds, s, occ);
+    if (ppt == 4) return pmd_one<FW, LPM, LAY, 4>(p, ext, lds, s, occ);
+    return pmd_one<FW, LPM, LAY, 1>(p, ext, lds, s, occ);
+}
+
+template <int FW, int LPM>
+hipError_t pmd_lay(const CopKPmd *p, int lay, int ppt, int ext, uint32_t lds, hipStream_t s, int *occ)
+{
+    if (lay == COPK_LAY_IMIX) return pmd_ppt<FW, LPM, COPK_LAY_IMIX>(p, ppt, ext, lds, s, occ);
+    if (lay == COPK_LAY_COALESCED) return pmd_ppt<FW, LPM, COPK_LAY_COALESCED>(p, ppt, ext, lds, s, occ);
+    if (lay == COPK_LAY_HDR16) return pmd_ppt<FW, LPM, COPK_LAY_HDR16>(p, ppt, ext, lds, s, occ);
+    return pmd_ppt<FW, LPM, COPK_LAY_SLOTS>(p, ppt, ext, lds, s, occ);
+}
+
+template <int FW>
+hipError_t pmd_lpm(const CopKPmd *p, int lpm, int lay, int ppt, int ext, uint32_t lds, hipStream_t s, int *occ)
+{
+    if (lpm == COPK_TBL_IVT) return pmd_lay<FW, COPK_TBL_IVT>(p, lay, ppt, ext, lds, s, occ);
+    if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);
+    return pmd_lay<FW, COPK_TBL_OFF>(p, lay, ppt, ext, lds, s, occ);
+}
+
+hipError_t pmd_dispatch(const CopKPmd *p, int fw, int lpm, int lay, int ppt, int ext, uint32_t lds, hipStream_t s,
+                        int *occ)
+{
+    if (fw == COPK_TBL_IVT) return pmd_lpm<COPK_TBL_IVT>(p, lpm, lay, ppt, ext, lds, s, occ);
+    if (fw == COPK_TBL_DIR) return pmd_lpm<COPK_TBL_DIR>(p, lpm, lay, ppt, ext, lds, s, occ);
+    return pmd_lpm<COPK_TBL_OFF>(p, lpm, lay, ppt, ext, lds, s, occ);
+}
+
+}  // namespace
+
+extern "C" hipError_t copk_pmd_launch(const CopKPmd *p, int fw_mode, int lpm_mode, int layout, int ppt, int ext,
+                                      uint32_t lds_bytes, hipStream_t stream)
+{
+    return pmd_dispatch(p, fw_mode, lpm_mode, layout, ppt, ext, lds_bytes, stream, nullptr);
+}
+
+extern "C" hipError_t copk_pmd_occupancy(int fw_mode, int lpm_mode, int layout, int ppt, int ext, uint32_t lds_bytes,
+                                         int *per_cu)
+{
+    *per_cu = 0;
+    return pmd_dispatch(nullptr, fw_mode, lpm_mode, layout, ppt, ext, lds_bytes, nullptr, per_cu);
+}

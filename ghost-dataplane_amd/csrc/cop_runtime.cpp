@@ -17,6 +17,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -218,6 +220,7 @@ struct cop_ctx {
         hipEvent_t done = nullptr;
         bool busy = false;
     } hs[COP_HOST_SLOTS];
+    cop_pmd *pmd = nullptr;             // the poll-mode kernel serving this context, if any
     hipStream_t tele_stream = nullptr;  // cop_counters_snapshot
     uint64_t *tele_host = nullptr;
     unsigned long long *tele_dev = nullptr;
@@ -297,6 +300,7 @@ static void coll_destroy(cop_ctx *c);
 void cop_destroy(cop_ctx *c)
 {
     if (!c) return;
+    if (c->pmd) (void)cop_pmd_stop(c->pmd);
     (void)hipSetDevice(c->device);
     for (int l = 0; l < MAX_LANES; l++)
         if (c->lane[l].s) (void)hipStreamSynchronize(c->lane[l].s);
@@ -385,6 +389,7 @@ static int take_lane_errors(cop_ctx *c, uint32_t mask)
 int cop_set_routing_table(cop_ctx *c, const uint16_t *rt)
 {
     if (!c || !rt) return -EINVAL;
+    if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel is serving this context (cop_pmd_stop first)");
     if (c->lane[0].s)
         if (int rc = sync_lanes(c)) return rc;
     HIPCHK(c, hipSetDevice(c->device));
@@ -609,6 +614,7 @@ static int resize_counters(cop_ctx *c, uint32_t n_rules)
 int cop_set_fw_table(cop_ctx *c, const cop_lpm_table *t)
 {
     if (!c || !t) return -EINVAL;
+    if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel is serving this context (cop_pmd_stop first)");
     if (t->n_rules > COP_LPM_NH_MASK) return set_err(c, -EINVAL, "rule ids exceed 24 bits");
     int rc = upload_lpm(c, c->fw, t, !(c->cfg.flags & COP_CFG_FW_FORCE_DIR24), COP_FORM_RULE);
     if (!rc && (c->cfg.flags & COP_CFG_RULE_COUNTERS)) rc = resize_counters(c, t->n_rules);
@@ -618,6 +624,7 @@ int cop_set_fw_table(cop_ctx *c, const cop_lpm_table *t)
 int cop_set_route_lpm(cop_ctx *c, const cop_lpm_table *t)
 {
     if (!c || !t) return -EINVAL;
+    if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel is serving this context (cop_pmd_stop first)");
     return upload_lpm(c, c->lpm, t, !(c->cfg.flags & COP_CFG_LPM_FORCE_DIR24), COP_FORM_NH);
 }
 
@@ -700,36 +707,17 @@ static Plan plan_launch(const cop_ctx *c, uint64_t total, bool imix, uint32_t mi
                                          : COPK_LAY_SLOTS};
 }
 
-// Fill the table / state part of the parameters and launch on lane L.
-// p.b / p.rg, p.nb, p.ntiles, p.uniform_ntiles, p.compact and p.stages are
-// set by the caller.
-static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uint32_t nb_used)
+// The table / counter / option part of a launch's parameters: table modes
+// (LDS interval form or HBM DIR-24-8, falling back to DIR-24-8 when LDS
+// would overflow), table pointers, the LDS carve, counters and options.
+// p.stages, p.compact and p.demux are set by the caller.
+static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int *lpm_mode_out, uint32_t *lds_out)
 {
-    const int ppt = pl.ppt;
     const uint32_t stages = p.stages;
     int fw_mode = pick_mode(c, c->fw, (stages & COP_STAGE_FW) != 0, (c->cfg.flags & COP_CFG_FW_FORCE_DIR24) != 0);
     int lpm_mode =
         pick_mode(c, c->lpm, (stages & COP_STAGE_LPM) != 0, (c->cfg.flags & COP_CFG_LPM_FORCE_DIR24) != 0);
-    HIPCHK(c, hipSetDevice(c->device));
-    // one chain per port (demux)
-    const uint32_t look_need = p.ntiles * (p.demux ? p.demux : 1u);
-    if (look_need > L.look_cap) {
-        // grow this lane's look-back words (stream order: free after its work)
-        HIPCHK(c, hipStreamSynchronize(L.s));
-        HIPCHK(c, hipFree(L.look));
-        L.look = nullptr;
-        L.look_cap = 0;
-        HIPCHK(c, hipMalloc(&L.look, (size_t)look_need * 8));
-        HIPCHK(c, memset_sync(L.look, 0, (size_t)look_need * 8, L.s));
-        L.look_cap = look_need;
-        L.epoch = 0;
-    }
     p.n_ports = c->cfg.n_ports;
-    if (++L.epoch == 0) {
-        HIPCHK(c, hipMemsetAsync(L.look, 0, (size_t)L.look_cap * 8, L.s));
-        L.epoch = 1;
-    }
-    p.epoch = L.epoch;
     p.dbg = c->dbg;
     p.rt_top = c->rt_top;
     p.rt_leaf = c->rt_leaf;
@@ -774,19 +762,53 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
         p.lds_stage_off = off;   // the tile's forward list, written out in 16-byte stores
         off += COPK_BLOCK * ppt;
     }
-    const uint32_t lds_bytes = off * 4 + c->lds_pad;
+    p.counters = c->counters;
+    p.rule_hits = (fw_mode != COPK_TBL_OFF && c->n_rule_ctr) ? c->counters + RULE_OFF : nullptr;
+    p.port_ctr = c->counters + SHARD_WORDS;
+    p.port_stats = (c->cfg.flags & COP_CFG_PORT_STATS) ? c->cfg.n_ports : 0u;
+    p.stamps = c->stamps;
+    *fw_mode_out = fw_mode;
+    *lpm_mode_out = lpm_mode;
+    *lds_out = off * 4 + c->lds_pad;
+    return 0;
+}
+
+// Launch the one-shot kernel on lane L: its look-back words and epoch, its
+// ticket buffers, then the table part (fill_launch).
+// p.b / p.rg, p.nb, p.ntiles, p.uniform_ntiles, p.compact, p.demux and
+// p.stages are set by the caller.
+static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uint32_t nb_used)
+{
+    const int ppt = pl.ppt;
+    HIPCHK(c, hipSetDevice(c->device));
+    // one chain per port (demux)
+    const uint32_t look_need = p.ntiles * (p.demux ? p.demux : 1u);
+    if (look_need > L.look_cap) {
+        // grow this lane's look-back words (stream order: free after its work)
+        HIPCHK(c, hipStreamSynchronize(L.s));
+        HIPCHK(c, hipFree(L.look));
+        L.look = nullptr;
+        L.look_cap = 0;
+        HIPCHK(c, hipMalloc(&L.look, (size_t)look_need * 8));
+        HIPCHK(c, memset_sync(L.look, 0, (size_t)look_need * 8, L.s));
+        L.look_cap = look_need;
+        L.epoch = 0;
+    }
+    int fw_mode = 0, lpm_mode = 0;
+    uint32_t lds_bytes = 0;
+    if (int rc = fill_launch(c, p, ppt, &fw_mode, &lpm_mode, &lds_bytes)) return rc;
+    if (++L.epoch == 0) {
+        HIPCHK(c, hipMemsetAsync(L.look, 0, (size_t)L.look_cap * 8, L.s));
+        L.epoch = 1;
+    }
+    p.epoch = L.epoch;
     // tickets: draw from buffer `parity`, zero the other buffer's dirty lines
     const int q = L.parity;
     p.tickets = L.tickets[q];
     p.zero_tickets = L.tickets[q ^ 1];
     p.zero_lines = L.dirty[q ^ 1];
     p.look = L.look;
-    p.counters = c->counters;
-    p.rule_hits = (fw_mode != COPK_TBL_OFF && c->n_rule_ctr) ? c->counters + RULE_OFF : nullptr;
-    p.port_ctr = c->counters + SHARD_WORDS;
-    p.port_stats = (c->cfg.flags & COP_CFG_PORT_STATS) ? c->cfg.n_ports : 0u;
     p.err = c->d_err + 4 * (&L - c->lane);
-    p.stamps = c->stamps;
     if ((c->dbg & 8u) && p.ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
     const uint32_t grid = p.ntiles;   // one tile per workgroup
 
@@ -1255,6 +1277,7 @@ int cop_port_stats_read(cop_ctx *c, cop_port_stats *out, uint32_t n, int reset)
 int cop_counters_snapshot(cop_ctx *c, cop_counters *total, cop_port_stats *ports, uint32_t n_ports, int reset)
 {
     if (!c || (n_ports && !ports)) return -EINVAL;
+    if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel holds the GPU (snapshot after cop_pmd_stop)");
     HIPCHK(c, hipSetDevice(c->device));
     if (!c->tele_stream) {
         HIPCHK(c, hipStreamCreateWithFlags(&c->tele_stream, hipStreamNonBlocking));
@@ -1483,6 +1506,355 @@ int cop_timer_stop(cop_ctx *c, double *ms)
     HIPCHK(c, hipEventElapsedTime(&f, c->t0, c->t1));
     *ms = f;
     return 0;
+}
+
+
+// ---- poll-mode kernel (cop_pmd.hip) ---------------------------------------
+// A persistent kernel serving one batch ring: the host posts batches by
+// bumping a counter in mapped host memory and reads their completion from
+// per-slot words the kernel writes there. No launch, no per-launch ramp,
+// tables staged into LDS once per worker.
+
+struct cop_pmd {
+    cop_ctx *c = nullptr;
+    hipStream_t s = nullptr;
+    CopKPmd P{};
+    int fw_mode = 0, lpm_mode = 0, layout = 0, ppt = 0, ext = 0;
+    uint32_t lds_bytes = 0;
+    uint8_t *ctl = nullptr;                 // mapped host control block
+    volatile uint64_t *h_posted = nullptr;
+    volatile uint32_t *h_stop = nullptr;
+    volatile uint32_t *h_state = nullptr;
+    volatile uint64_t *h_done = nullptr;
+    uint8_t *dev = nullptr;                 // device words: relay, ctl, slot tile counts, look-back
+    size_t dev_bytes = 0;
+    uint64_t posted = 0, completed = 0;
+    uint32_t n_slots = 0, tpb = 0, per_cu = 0;
+    uint32_t launches = 0;
+    bool live = false;                      // a launch may still be running
+};
+
+static int pmd_launch(cop_pmd *m, uint64_t seq0)
+{
+    cop_ctx *c = m->c;
+    HIPCHK(c, hipSetDevice(c->device));
+    // device control words (d_posted, d_ctl) restart at 0; the slot tile
+    // counts carry over (every served batch completed: multiples of tpb)
+    HIPCHK(c, hipMemsetAsync(m->dev, 0, 64, m->s));
+    m->h_state[0] = 0;
+    m->h_state[1] = 0;
+    *m->h_stop = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    m->P.seq0 = seq0;
+    hipError_t e = copk_pmd_launch(&m->P, m->fw_mode, m->lpm_mode, m->layout, m->ppt, m->ext, m->lds_bytes, m->s);
+    if (e != hipSuccess) return set_err(c, -EIO, "pmd launch: %s", hipGetErrorString(e));
+    m->launches++;
+    m->live = true;
+    return 0;
+}
+
+// wait until the launch has left the GPU (bounded: it leaves by itself on
+// stop, idle or abort)
+static int pmd_join(cop_pmd *m, double timeout_s)
+{
+    if (!m->live) return 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        hipError_t e = hipStreamQuery(m->s);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return set_err(m->c, -EIO, "pmd: %s", hipGetErrorString(e));
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+            return set_err(m->c, -ETIMEDOUT, "pmd: kernel did not leave within %.0f s", timeout_s);
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    m->live = false;
+    return 0;
+}
+
+// advance m->completed over the slots' completion words
+static void pmd_refresh(cop_pmd *m)
+{
+    while (m->completed < m->posted && m->h_done[m->completed % m->n_slots] == m->completed + 1) m->completed++;
+}
+
+static int pmd_census(cop_pmd *m);
+
+// the kernel left: relaunch after an idle exit (every batch it saw is
+// complete; posts it never saw start the new launch), else fail
+static int pmd_revive(cop_pmd *m)
+{
+    const uint32_t why = m->h_state[0];
+    if (why == COPK_PMD_RUNNING) return 0;
+    if (why != COPK_PMD_IDLE) return set_err(m->c, -EIO, "pmd kernel left (%s)", why == COPK_PMD_ABORT ?
+                                             "abort: workers not co-resident, or a look-back timed out" : "stopped");
+    if (int rc = pmd_join(m, 10.0)) return rc;
+    pmd_refresh(m);
+    if (int rc = pmd_launch(m, m->completed)) return rc;
+    const int st = pmd_census(m);
+    return st == 0 ? 0 : st < 0 ? st : set_err(m->c, -EIO, "pmd: workers never co-resident on relaunch");
+}
+
+// every worker must be resident at once (static tile order): all of the
+// GPU's workgroup slots for this kernel; other kernels on the device wait
+// until the poll-mode kernel stops or leaves idle
+static void pmd_size(cop_pmd *m)
+{
+    m->P.n_work = (uint32_t)m->c->ncu * m->per_cu;
+    m->P.relay_stride = 64;   // ~20 doorbell readers over PCIe
+}
+
+// wait for the launch's census: 0 = every worker resident, 1 = aborted
+// (some could not be), or -errno
+static int pmd_census(cop_pmd *m)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        if (m->h_state[1] == m->P.n_work) return 0;
+        if (m->h_state[0] == COPK_PMD_ABORT) return 1;
+        if (m->h_state[0] != COPK_PMD_RUNNING) return set_err(m->c, -EIO, "pmd: left during the census");
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 5.0)
+            return set_err(m->c, -ETIMEDOUT, "pmd: no census after 5 s");
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
+{
+    if (!c || !r || !out) return -EINVAL;
+    *out = nullptr;
+    if (c->pmd) return set_err(c, -EBUSY, "this context already has a poll-mode kernel");
+    if (r->n_slots == 0 || r->n == 0 || !r->pkts || !r->results) return set_err(c, -EINVAL, "pmd: empty ring");
+    if (r->n > c->cfg.max_batch) return set_err(c, -EINVAL, "pmd: n %u > max_batch", r->n);
+    const bool imix = r->offsets != nullptr;
+    if (((uintptr_t)r->pkts & 15) || (r->pkts_slot_bytes & 15) || (r->data_off & 15) ||
+        (!imix && ((r->stride & 15) || (r->stride < 36 && r->stride != COP_HDR16_STRIDE))))
+        return set_err(c, -EINVAL, "pmd: packet starts must be 16-byte aligned");
+    const bool compact = (r->fwd_idx || r->fwd_count) && !(c->cfg.flags & COP_CFG_NO_COMPACT);
+    const uint32_t lists = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 1u;
+    if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < (uint64_t)r->n * lists))
+        return set_err(c, -EINVAL, "pmd: slot sizes smaller than n (x ports with demux)");
+    if (int rc = sync_lanes(c)) return rc;
+
+    cop_pmd *m = new (std::nothrow) cop_pmd();
+    if (!m) return -ENOMEM;
+    m->c = c;
+    Plan pl = plan_launch(c, (uint64_t)r->n * r->n_slots, imix, r->stride);
+    // tile size: 1024-packet tiles (five workers per CU, so a 20-batch burst
+    // of 64k packets is one tile per worker), 256-packet tiles for small
+    // batches
+    int ppt = r->n >= 4u * COPK_BLOCK * 4 ? 4 : 1;
+    if (c->ppt_override) ppt = c->ppt_override;
+    pl.ppt = ppt;
+    m->ppt = ppt;
+    m->layout = pl.layout;
+    m->tpb = (r->n + COPK_BLOCK * ppt - 1) / (COPK_BLOCK * ppt);
+    m->n_slots = r->n_slots;
+    CopKParams &p = m->P.k;
+    memset(&p, 0, sizeof(p));
+    p.ring = 1;
+    p.rg.pkts = (const uint8_t *)r->pkts;
+    p.rg.offsets = r->offsets;
+    p.rg.results = r->results;
+    p.rg.fwd_idx = compact ? r->fwd_idx : nullptr;
+    p.rg.fwd_count = compact ? r->fwd_count : nullptr;
+    p.rg.pkts_slot_bytes = r->pkts_slot_bytes;
+    p.rg.offsets_slot_words = r->offsets_slot_words;
+    p.rg.results_slot = r->results_slot;
+    p.rg.fwd_slot = r->fwd_slot;
+    p.rg.n_slots = r->n_slots;
+    p.rg.first = 0;
+    p.rg.n = r->n;
+    p.rg.stride = r->stride;
+    p.rg.data_off = r->data_off;
+    p.nb = 1;
+    p.ntiles = m->tpb;
+    p.uniform_ntiles = m->tpb;
+    p.compact = compact ? 1u : 0u;
+    p.stages = c->cfg.stages;
+    p.demux = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 0u;
+    int rc = 0;
+#define PMD_FAIL(code)       \
+    do {                     \
+        rc = (code);         \
+        goto fail;           \
+    } while (0)
+    {
+        if ((rc = fill_launch(c, p, ppt, &m->fw_mode, &m->lpm_mode, &m->lds_bytes))) goto fail;
+        p.dbg = 0;   // no ablations in the persistent kernel
+        p.stamps = nullptr;
+        const bool stamps = getenv("COP_PMD_STAMPS") != nullptr;
+        if (stamps) {   // diagnostic: the tile body's phase stamps too (EXT kernel)
+            if (hipMalloc(&p.stamps, (size_t)c->ncu * 8 * 8 * 8) != hipSuccess)
+                PMD_FAIL(set_err(c, -ENOMEM, "pmd: stamps"));
+            p.dbg = 8;
+        }
+        m->ext = (p.demux || p.port_stats || p.rule_hits || p.dbg) ? 1 : 0;
+        int occ = 0;
+        hipError_t e = copk_pmd_occupancy(m->fw_mode, m->lpm_mode, m->layout, ppt, m->ext, m->lds_bytes, &occ);
+        if (e != hipSuccess || occ < 1) PMD_FAIL(set_err(c, -EIO, "pmd occupancy: %s (%d)", hipGetErrorString(e), occ));
+        // the hardware admits at most 800 / (roundup16(sgprs) + 16) 256-thread
+        // workgroups per CU (MI355X_MICROARCH.md, Residency): 6 at the
+        // pipeline kernels' ~106 SGPRs, below what the API may answer; the
+        // start-up census confirms, else one fewer per CU is tried
+        occ = std::min(occ, 6);
+        if (getenv("COP_PMD_STAMPS")) occ = std::min(occ, 4);   // the EXT diagnostic kernel holds more registers
+        if (const char *env = getenv("COP_PMD_PER_CU")) occ = std::min(occ, std::max(1, atoi(env)));
+        m->per_cu = (uint32_t)occ;
+        pmd_size(m);
+        m->P.idle_ticks = 100000000u;   // 1 s at 100 MHz
+        if (const char *env = getenv("COP_PMD_IDLE_MS")) m->P.idle_ticks = (uint32_t)strtoul(env, nullptr, 0) * 100000u;
+        // control block in mapped host memory
+        const size_t ctl_bytes = 64 + (size_t)m->n_slots * 8;
+        HIPCHK(c, hipSetDevice(c->device));
+        if (hipHostMalloc(&m->ctl, ctl_bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            PMD_FAIL(set_err(c, -ENOMEM, "pmd: host control block"));
+        memset(m->ctl, 0, ctl_bytes);
+        void *dctl = nullptr;
+        if (hipHostGetDevicePointer(&dctl, m->ctl, 0) != hipSuccess) PMD_FAIL(set_err(c, -EIO, "pmd: mapping"));
+        m->h_posted = (volatile uint64_t *)m->ctl;
+        m->h_stop = (volatile uint32_t *)(m->ctl + 8);
+        m->h_state = (volatile uint32_t *)(m->ctl + 16);
+        m->h_done = (volatile uint64_t *)(m->ctl + 64);
+        m->P.h_posted = (const unsigned long long *)dctl;
+        m->P.h_stop = (const uint32_t *)((uint8_t *)dctl + 8);
+        m->P.h_state = (uint32_t *)((uint8_t *)dctl + 16);
+        m->P.h_done = (unsigned long long *)((uint8_t *)dctl + 64);
+        // device words: [0] relay, [8] ctl, [64] slot tile counts, then look-back
+        const size_t look_off = (64 + (size_t)m->n_slots * 8 + 255) & ~(size_t)255;
+        const size_t look_words = (size_t)m->n_slots * m->tpb * (p.demux ? p.demux : 1u);
+        m->dev_bytes = look_off + look_words * 8;
+        if (getenv("COP_PMD_STAMPS")) {   // diagnostic phase stamps (cop_debug_pmd_stamps)
+            if (hipMalloc(&m->P.stamps, ((size_t)m->P.n_work * 8 + 128) * 8) != hipSuccess)
+                PMD_FAIL(set_err(c, -ENOMEM, "pmd: stamps"));
+            (void)hipMemset(m->P.stamps, 0, ((size_t)m->P.n_work * 8 + 128) * 8);
+            (void)hipDeviceSynchronize();
+        }
+        if (hipMalloc(&m->dev, m->dev_bytes) != hipSuccess) PMD_FAIL(set_err(c, -ENOMEM, "pmd: device words"));
+        if (hipStreamCreateWithFlags(&m->s, hipStreamNonBlocking) != hipSuccess)
+            PMD_FAIL(set_err(c, -EIO, "pmd: stream"));
+        if (memset_sync(m->dev, 0, m->dev_bytes, m->s) != hipSuccess) PMD_FAIL(set_err(c, -EIO, "pmd: memset"));
+        m->P.d_posted = (unsigned long long *)m->dev;
+        m->P.d_ctl = (uint32_t *)(m->dev + 8);
+        m->P.slot_tiles = (unsigned long long *)(m->dev + 64);
+        p.look = (unsigned long long *)(m->dev + look_off);
+        p.err = nullptr;   // the look-back reports through d_ctl[2] (LookCtx)
+        p.epoch = 0;
+        // launch; if the census finds workers that could not become
+        // resident, retry with one workgroup fewer per CU
+        for (;;) {
+            if ((rc = pmd_launch(m, 0))) goto fail;
+            const int st = pmd_census(m);
+            if (st == 0) break;
+            if (st < 0 || m->per_cu <= 1) PMD_FAIL(st < 0 ? st : set_err(c, -EIO, "pmd: workers never co-resident"));
+            if ((rc = pmd_join(m, 10.0))) goto fail;
+            m->per_cu--;
+            pmd_size(m);
+        }
+    }
+#undef PMD_FAIL
+    c->pmd = m;
+    *out = m;
+    return 0;
+fail:
+    if (m->P.stamps) (void)hipFree(m->P.stamps);
+    if (m->P.k.stamps) (void)hipFree(m->P.k.stamps);
+    if (m->s) (void)hipStreamDestroy(m->s);
+    if (m->dev) (void)hipFree(m->dev);
+    if (m->ctl) (void)hipHostFree(m->ctl);
+    delete m;
+    return rc;
+}
+
+int cop_pmd_post(cop_pmd *m, uint32_t count)
+{
+    if (!m) return -EINVAL;
+    if (count == 0) return 0;
+    if (count > m->n_slots) return set_err(m->c, -EINVAL, "pmd: post of %u > %u ring slots", count, m->n_slots);
+    // a slot is reposted only after its previous batch completed
+    const uint64_t need = m->posted + count;
+    if (need - m->completed > m->n_slots)
+        if (int rc = cop_pmd_wait(m, need - m->n_slots)) return rc;
+    if (int rc = pmd_revive(m)) return rc;
+    std::atomic_thread_fence(std::memory_order_seq_cst);   // ring slots written before the doorbell
+    *m->h_posted = need;
+    m->posted = need;
+    return 0;
+}
+
+int cop_pmd_wait(cop_pmd *m, uint64_t seq)
+{
+    if (!m) return -EINVAL;
+    if (seq > m->posted) return set_err(m->c, -EINVAL, "pmd: wait for %llu > %llu posted", (unsigned long long)seq,
+                                        (unsigned long long)m->posted);
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t spins = 0;
+    for (;;) {
+        pmd_refresh(m);
+        if (m->completed >= seq) break;
+        if (m->h_state[0] != COPK_PMD_RUNNING) {
+            pmd_refresh(m);   // its last completion may have landed just before it left
+            if (m->completed >= seq) break;
+            if (int rc = pmd_revive(m)) return rc;
+        }
+        if ((++spins & 1023u) == 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 30.0)
+            return set_err(m->c, -ETIMEDOUT, "pmd: batch %llu not complete after 30 s",
+                           (unsigned long long)m->completed);
+    }
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    return 0;
+}
+
+uint64_t cop_pmd_posted(const cop_pmd *m) { return m ? m->posted : 0; }
+
+int cop_pmd_info(const cop_pmd *m, cop_pmd_info_t *out)
+{
+    if (!m || !out) return -EINVAL;
+    out->workers = m->P.n_work;
+    out->workers_per_cu = m->per_cu;
+    out->tiles_per_batch = m->tpb;
+    out->packets_per_tile = COPK_BLOCK * (uint32_t)m->ppt;
+    out->launches = m->launches;
+    out->state = m->h_state[0];
+    out->posted = m->posted;
+    out->completed = m->completed;
+    return 0;
+}
+
+int cop_pmd_stop(cop_pmd *m)
+{
+    if (!m) return -EINVAL;
+    cop_ctx *c = m->c;
+    int rc = cop_pmd_wait(m, m->posted);
+    *m->h_stop = 1;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    const int jrc = pmd_join(m, 10.0);
+    if (!rc) rc = jrc;
+    if (!jrc) {
+        if (m->s) (void)hipStreamDestroy(m->s);
+        if (m->dev) (void)hipFree(m->dev);
+        if (m->ctl) (void)hipHostFree(m->ctl);
+        if (m->P.stamps) (void)hipFree(m->P.stamps);
+        if (m->P.k.stamps) (void)hipFree(m->P.k.stamps);
+    }   // else: the kernel may still touch them; leak rather than free under it
+    if (c->pmd == m) c->pmd = nullptr;
+    delete m;
+    return rc;
+}
+
+/* diagnostic (not in the public header): the poll-mode kernel's phase
+ * stamps ($COP_PMD_STAMPS): per worker 8 u64 {tile start, batch seen,
+ * body done, counted, batch, last-of-batch, -, -}, then 64 doorbell relays
+ * {posted, time}; s_memrealtime ticks (100 MHz). Returns words copied. */
+int cop_debug_pmd_stamps(cop_pmd *m, uint64_t *out, uint32_t max_words)
+{
+    if (!m || !m->P.stamps || !out) return -EINVAL;
+    const uint32_t n = std::min<uint32_t>(max_words, m->P.n_work * 8 + 128);
+    HIPCHK(m->c, hipMemcpy(out, m->P.stamps, (size_t)n * 8, hipMemcpyDeviceToHost));
+    // then the tile body's stamps (cop_tile.h STAMP: 2 pass 1, 3 pass 2, 5 compaction, 6 counters)
+    const uint32_t n2 = std::min<uint32_t>(max_words - n, m->P.n_work * 8);
+    if (n2 && m->P.k.stamps) HIPCHK(m->c, hipMemcpy(out + n, m->P.k.stamps, (size_t)n2 * 8, hipMemcpyDeviceToHost));
+    return (int)(n + (m->P.k.stamps ? n2 : 0));
 }
 
 /* test hook (not in the public header): make the next `count` launches

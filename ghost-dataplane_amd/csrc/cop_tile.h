@@ -1,0 +1,179 @@
+// cop_tile.h — the per-tile pipeline body shared by the one-shot kernel
+// (cop_kernels.hip) and the poll-mode kernel (cop_pmd.hip). Internal.
+#ifndef COP_TILE_H
+#define COP_TILE_H
+
+#include "cop_device.h"
+
+namespace copd {
+
+// diagnostic-only phase stamps (p.dbg bit 8): wave 0 lane 0 writes
+// s_memrealtime (100 MHz) per phase into a buffer nothing else reads
+#define STAMP(ph)                                                                          \
+    do {                                                                                   \
+        if ((o.dbg & 8u) && tid == 0) {                                                    \
+            __builtin_amdgcn_sched_barrier(0);                                             \
+            __hip_atomic_store(&p.stamps[blockIdx.x * 8 + (ph)], __builtin_amdgcn_s_memrealtime(), \
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                     \
+            __builtin_amdgcn_sched_barrier(0);                                             \
+        }                                                                                  \
+    } while (0)
+
+// LDS carve of a launch (offsets in u32 words, all multiples of 4): the
+// staged tables, then the misc scratch (compaction counts and prefixes, the
+// ticket broadcast, counter reduction, per-port scratch), then the tile's
+// staged forward list.
+struct LdsCarve {
+    Tables tb;
+    CompactLds cl;
+    uint32_t *s_tile;   // ticket broadcast
+    uint32_t *s_red;    // [WAVES][8] counter reduction
+    uint32_t *s_ps;     // [WAVES][16] per-port counter reduction
+    uint32_t *s_misc;   // the misc area (poll-mode kernel: doorbell broadcast at +36)
+};
+
+template <int PPT>
+__device__ __forceinline__ LdsCarve lds_carve(const CopKParams &p, uint32_t *lds)
+{
+    LdsCarve c;
+    c.tb.rt_top = lds;                                  // 256
+    c.tb.rt_leaf = (uint16_t *)(lds + 256);       // nleaf*256 u16
+    c.tb.fw_s = lds + p.lds_fw_off;
+    c.tb.fw_v = c.tb.fw_s + p.fw_m;
+    c.tb.lp_s = lds + p.lds_lpm_off;
+    c.tb.lp_v = c.tb.lp_s + p.lpm_m;
+    uint32_t *misc = lds + p.lds_misc_off;
+    c.s_misc = misc;
+    c.s_tile = misc + 32;
+    c.s_red = misc + 40;                                            // [WAVES][8]
+    c.cl.cnt = misc;                                                // [PPT*WAVES]
+    c.cl.pref = misc + 33;
+    c.cl.dq = misc + COPK_LDS_MISC_WORDS;                           // [K][PPT*WAVES]
+    c.cl.dpref = c.cl.dq + COPK_MAX_DEMUX_PORTS * PPT * WAVES;      // [K]
+    c.s_ps = c.cl.dpref + 8;                                        // [WAVES][16]
+    c.cl.stage = p.lds_stage_off ? lds + p.lds_stage_off : nullptr; // [TILE]
+    return c;
+}
+
+// Stage the vport route image and the interval tables into LDS by LDS-DMA
+// (completion: the caller's __syncthreads()).
+template <int FW, int LPM>
+__device__ __forceinline__ void stage_tables(const CopKParams &p, const Tables &tb, int lane, int wave)
+{
+    lds_stage(tb.rt_top, p.rt_top, 64, lane, wave);
+    lds_stage((uint32_t *)tb.rt_leaf, p.rt_leaf, p.rt_nleaf * 32u, lane, wave);
+    if (FW == COPK_TBL_IVT) {
+        lds_stage(tb.fw_s, p.fw_starts, p.fw_m >> 2, lane, wave);
+        lds_stage(tb.fw_v, p.fw_vals, p.fw_m >> 2, lane, wave);
+    }
+    if (LPM == COPK_TBL_IVT) {
+        lds_stage(tb.lp_s, p.lpm_starts, p.lpm_m >> 2, lane, wave);
+        lds_stage(tb.lp_v, p.lpm_vals, p.lpm_m >> 2, lane, wave);
+    }
+}
+
+// One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,
+// parse/route, lookups, verdicts, records, ordered compaction and the
+// counter flush. Shared by the one-shot kernel (one tile per workgroup)
+// and the poll-mode kernel (cop_pmd.hip: a persistent loop over tiles).
+// WT: write-through output stores (poll-mode). sync_tables: wait for the
+// LDS-DMA table staging after the header loads are issued.
+template <int FW, int LPM, int LAY, int PPT, bool EXT, bool WT>
+__device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, const LdsCarve &lc, const CopKBatch &B,
+                                          uint32_t look_off, uint32_t j, const LookCtx &lk, int tid, int lane, int wave,
+                                          bool sync_tables)
+{
+    constexpr bool IMIX = LAY == COPK_LAY_IMIX;
+    const Tables &tb = lc.tb;
+    constexpr int TILE = BLOCK * PPT;
+    const uint32_t base = j * TILE;
+    // ---- packet header loads (all PPT packets, no branches). Lanes past
+    // the end of the batch re-read the last packet and are masked out of
+    // every store and count. ----
+    uint32_t w3[PPT], w6[PPT], w7[PPT], w8[PPT];
+    bool valid[PPT];
+    const uint32_t last = B.n ? B.n - 1 : 0u;
+    if (LAY == COPK_LAY_COALESCED && B.n) {
+        const StepGeom sg = step_geom(lane);
+        u32x4 v[PPT][3];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
+#pragma unroll
+        for (int k = 0; k < PPT; k++) gather_step(sg, v[k], w3[k], w6[k], w7[k], w8[k]);
+    } else if (LAY == COPK_LAY_HDR16 && B.n) {
+        // one 16-byte record per packet: frame bytes 12..15 then 24..35
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const uint32_t ic = min(base + k * BLOCK + tid, last);
+            const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(B.pkts + B.data_off + (size_t)ic * 16u));
+            w3[k] = v.x;
+            w6[k] = v.y;
+            w7[k] = v.z;
+            w8[k] = v.w;
+        }
+    } else if (B.n) {
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const uint32_t ic = min(base + k * BLOCK + tid, last);
+            const uint8_t *pk;
+            if (IMIX) pk = B.pkts + B.offsets[ic] + B.data_off;
+            else pk = B.pkts + (size_t)ic * B.stride + B.data_off;
+            // two loads: bytes 12..27 (dwordx4 at a 4-byte-aligned address;
+            // w3 and w6) and 28..35 (w7, w8)
+            const u32x4a a = *(const u32x4a *)(pk + 12);
+            const u32x2a b = *(const u32x2a *)(pk + 28);
+            w3[k] = a.x;
+            w6[k] = a.w;
+            w7[k] = b.x;
+            w8[k] = b.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < PPT; k++) w3[k] = w6[k] = w7[k] = w8[k] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < PPT; k++) valid[k] = base + k * BLOCK + tid < B.n;
+    if (sync_tables) __syncthreads();   // LDS-DMA table staging has landed
+
+    // ---- pass 1 (parse, route, LDS searches, tbl24 loads issued) ----
+    uint32_t verdict[PPT], port[PPT], flags[PPT], rnh[PPT], fwe[PPT], lpe[PPT], src[PPT], dst[PPT];
+    pass1<FW, LPM, PPT>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe);
+    if (o.dbg & 8u) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) x ^= verdict[k] ^ src[k];
+        asm volatile("" ::"v"(x));
+    }
+    STAMP(2);
+
+    // ---- pass 2 (tbl8 step) and the verdicts ----
+    Counts cn;
+    pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, cn.total, cn.notv4);
+    rule_hit_atomics<FW, PPT>(o, valid, flags, fwe);
+    if (o.dbg & 8u) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) x ^= verdict[k] ^ rnh[k];
+        asm volatile("" ::"v"(x));
+    }
+    STAMP(3);
+    // ---- ordered compaction (one list per batch, or per vport), with the
+    // result records (8 B per packet, coalesced) stored during its look-back
+    bool fwd[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) fwd[k] = valid[k] && verdict[k] == COPK_FORWARD;
+    auto records = [&] { store_records<PPT, WT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn); };
+    if (p.compact) compact_tile<PPT, WT>(lk, o, B, look_off, j, base, fwd, port, lc.cl, tid, lane, wave, records);
+    else records();
+    STAMP(5);
+
+    // ---- counters (one flush per workgroup) ----
+    uint32_t prx[COPK_MAX_DEMUX_PORTS] = {}, ptx[COPK_MAX_DEMUX_PORTS] = {};
+    if (o.port_stats) port_counts<PPT>(o.port_stats, valid, fwd, port, prx, ptx);
+    flush_counters(p, o, cn, prx, ptx, lc.s_red, lc.s_ps, tid, lane, wave);
+    STAMP(6);
+}
+
+}  // namespace copd
+
+#endif

@@ -332,6 +332,48 @@ int  cop_set_host_threads(cop_ctx *ctx, uint32_t n);
 int  cop_host_batch_submit(cop_ctx *ctx, uint32_t slot, const void *const *pkt_data, uint32_t n);
 int  cop_host_batch_wait(cop_ctx *ctx, uint32_t slot, const cop_result **results, uint32_t *n);
 
+/* ------------------------------------------------------------------------ */
+/* Poll-mode coprocessor: a persistent kernel serving a batch ring          */
+/* ------------------------------------------------------------------------ */
+
+/* The GPU form of the reference's coprocessor lcores, which poll their rx
+ * rings forever (main_loop -> coprocessor(), switch.c:529-535) rather than
+ * being started per burst. cop_pmd_start launches ONE long-lived kernel on
+ * its own stream that serves `ring` (a batch ring in HBM, as for
+ * cop_submit_ring) until cop_pmd_stop: the host posts batches by bumping a
+ * doorbell counter in mapped host memory, and the kernel writes each batch's
+ * completion back there. Batch sequence number b (0, 1, 2, ... in post
+ * order) lives in ring slot b % n_slots; per-batch outputs and counters are
+ * exactly those of cop_submit_ring. No launch per post: no launch latency,
+ * no grid ramp, tables staged into LDS once.
+ * While it runs, the context's tables cannot change (-EBUSY) and it holds
+ * nearly every workgroup slot of the GPU (other launches on the context
+ * still run, slowly). One per context. The kernel leaves by itself after 1 s
+ * without a post ($COP_PMD_IDLE_MS) and is relaunched by the next post. */
+typedef struct cop_pmd cop_pmd;
+int cop_pmd_start(cop_ctx *ctx, const cop_batch_ring *ring, cop_pmd **out);
+/* Post the next `count` batches (<= n_slots): sequence numbers posted ..
+ * posted+count-1. Blocks while that would reuse a slot whose batch has not
+ * completed. 0 or -errno. */
+int cop_pmd_post(cop_pmd *pmd, uint32_t count);
+/* Spin until every batch with sequence number < seq has completed: records,
+ * forward lists and counts are in HBM, visible to the host and to later
+ * kernels. 0, -ETIMEDOUT (30 s) or -EIO (the kernel aborted). */
+int cop_pmd_wait(cop_pmd *pmd, uint64_t seq);
+uint64_t cop_pmd_posted(const cop_pmd *pmd);
+typedef struct cop_pmd_info_t {
+    uint32_t workers;          /* worker workgroups (all co-resident) */
+    uint32_t workers_per_cu;
+    uint32_t tiles_per_batch;
+    uint32_t packets_per_tile;
+    uint32_t launches;         /* 1 + relaunches after idle exits */
+    uint32_t state;            /* 0 running, 1 stopped, 2 left idle, 3 aborted */
+    uint64_t posted, completed;
+} cop_pmd_info_t;
+int cop_pmd_info(const cop_pmd *pmd, cop_pmd_info_t *out);
+/* Complete everything posted, stop the kernel, free. */
+int cop_pmd_stop(cop_pmd *pmd);
+
 /* Counters (u64, device-resident, summed over every submitted packet).
  * On the device they are kept in COP_COUNTER_SHARDS shards of
  * COP_N_COUNTERS words (one 128-byte line each, to spread the atomics);

@@ -1,0 +1,280 @@
+"""The poll-mode (persistent) kernel, cop_pmd_* (csrc/cop_pmd.hip): one
+long-lived launch serving a batch ring, batches posted through a host
+doorbell. Every record, forward list and count must equal the oracle's, as
+for the one-shot launches (test_gpu_ring.py), across: posts of one batch
+and of many, ring wrap-around with slot reuse, every packet layout
+(coalesced 64 B slots, mbuf stride with headroom, 16-byte header records,
+IMIX), the DIR-24-8 stages, per-rule counters, demux and port statistics,
+an idle exit followed by a relaunch, and stop/restart on one context."""
+import time
+
+import numpy as np
+import pytest
+
+import copgpu as cg
+import oracle as orc
+from helpers import oracle_tables
+
+pytestmark = pytest.mark.gpu
+
+S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
+
+
+def fw1k(seed=0x5EED1002):
+    return cg.gen_rules(seed, 1000, cg.GEN_FW, 20)
+
+
+def routes(n=100000, seed=0x5EED2004):
+    return cg.gen_rules(seed, n, cg.GEN_ROUTES, 0)
+
+
+class Ring:
+    """P slots of B packets in HBM (64 B slots unless stride/data_off say
+    otherwise), with records, forward lists (x lists) and counts."""
+
+    def __init__(self, ctx, pk, B, P, stride=64, data_off=0, lists=1):
+        self.B, self.P, self.lists = B, P, lists
+        self.slot_bytes = ((B * stride + data_off + 4095) // 4096) * 4096
+        self.dp = ctx.alloc(self.slot_bytes * P)
+        for s in range(P):
+            if stride == 64 and data_off == 0:
+                self.dp.upload(pk[s * B * 64:(s + 1) * B * 64], s * self.slot_bytes)
+            else:
+                buf = np.zeros(self.slot_bytes, np.uint8)
+                v = buf[data_off:data_off + B * stride].reshape(B, stride)
+                v[:, :min(64, stride)] = pk[s * B * 64:(s + 1) * B * 64].reshape(B, 64)[:, :min(64, stride)]
+                self.dp.upload(buf, s * self.slot_bytes)
+        self.dr = ctx.alloc(B * P * 8)
+        self.df = ctx.alloc(B * P * 4 * lists)
+        self.dc = ctx.alloc(P * 4 * lists)
+        self.dr.fill(0xAB)
+        self.dc.fill(0xFF)
+        self.ring = cg.make_ring(self.dp, P, B, self.dr, self.slot_bytes, stride=stride, data_off=data_off,
+                                 fwd_idx=self.df, fwd_slot=B * lists, fwd_count=self.dc)
+
+    def read(self):
+        return (self.dr.download(cg.RESULT_DT, self.B * self.P), self.df.download(np.uint32, self.B * self.P * self.lists),
+                self.dc.download(np.uint32, self.P * self.lists))
+
+
+def oracle_slots(pk, B, P, stages, fw, rt=None):
+    recs, fos = [], []
+    for s in range(P):
+        r, f, _ = orc.process(pk[s * B * 64:(s + 1) * B * 64], B, stages=stages, fw=fw, route=rt)
+        recs.append(r)
+        fos.append(f)
+    return np.concatenate(recs), fos
+
+
+def check(res, fwd, cnt, ro, fos, B, P):
+    for s in range(P):
+        assert np.array_equal(res[s * B:(s + 1) * B].view(np.uint8), ro[s * B:(s + 1) * B].view(np.uint8)), \
+            f"slot {s} records"
+        c = int(cnt[s])
+        assert c == len(fos[s]), f"slot {s} count"
+        assert np.array_equal(fwd[s * B:s * B + c], fos[s]), f"slot {s} forward list"
+
+
+def test_pmd_fw1k_posts_and_wraparound(gpu_ctx_factory):
+    """The bench's shape (64k-packet slots): one post of every slot, then
+    posts of 1, 7 and 24 that wrap the ring and reuse slots (each slot's
+    outputs are rewritten identically); counters sum every posted batch."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    B, P = 65536, 24
+    pk = cg.gen_trace(0x5EED0B00, B * P, rules)
+    fw, _ = oracle_tables(rules)
+    ro, fos = oracle_slots(pk, B, P, S | F, fw)
+    rg = Ring(ctx, pk, B, P)
+    with ctx.pmd_start(rg.ring) as m:
+        info = m.info()
+        assert info["tiles_per_batch"] * info["packets_per_tile"] >= B and info["workers"] >= 256
+        assert info["state"] == 0 and info["launches"] == 1
+        m.post(P)
+        m.wait()
+        check(*rg.read(), ro, fos, B, P)
+        rg.dr.fill(0xAB)
+        rg.dc.fill(0xFF)
+        total = P
+        for k in (1, 7, 24, 24, 3):
+            m.post(k)
+            total += k
+        m.wait()
+        assert m.posted == total
+        check(*rg.read(), ro, fos, B, P)
+    c = ctx.counters()
+    assert c["rx"] == total * B
+    assert c["forward"] == sum(len(fos[b % P]) for b in range(total))   # batch b ran in slot b % P
+
+
+def test_pmd_one_batch_at_a_time(gpu_ctx_factory):
+    """Post, wait, post, wait: the doorbell path with nothing queued (the
+    workers idle between posts, the relay wakes them)."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    B, P = 65536, 5
+    pk = cg.gen_trace(0x5EED0B10, B * P, rules)
+    fw, _ = oracle_tables(rules)
+    ro, fos = oracle_slots(pk, B, P, S | F, fw)
+    rg = Ring(ctx, pk, B, P)
+    m = ctx.pmd_start(rg.ring)
+    for i in range(40):
+        m.post(1)
+        m.wait(i + 1)
+        if i == P - 1:
+            check(*rg.read(), ro, fos, B, P)
+    m.stop()
+    check(*rg.read(), ro, fos, B, P)
+    assert ctx.counters()["rx"] == 40 * B
+
+
+@pytest.mark.parametrize("layout", ["mbuf", "hdr16", "small"])
+def test_pmd_layouts(gpu_ctx_factory, layout):
+    """Packets at mbuf stride (2176 B, 128 B headroom), as 16-byte header
+    records, and small batches (a few tiles of 256 or 1024 packets)."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    B, P = (30000 + 5, 4) if layout != "small" else (5000 + 3, 9)
+    pk = cg.gen_trace(0x5EED0B20, B * P, rules)
+    fw, _ = oracle_tables(rules)
+    ro, fos = oracle_slots(pk, B, P, S | F, fw)
+    if layout == "hdr16":
+        rec = np.zeros((B * P, 16), np.uint8)
+        fr = pk.reshape(B * P, 64)
+        rec[:, 0:4] = fr[:, 12:16]
+        rec[:, 4:16] = fr[:, 24:36]
+        hp = np.zeros(B * P * 64, np.uint8)
+        hp.reshape(B * P, 64)[:, :16] = rec
+        rg = Ring(ctx, hp, B, P, stride=16)
+    elif layout == "mbuf":
+        rg = Ring(ctx, pk, B, P, stride=2176, data_off=128)
+    else:
+        rg = Ring(ctx, pk, B, P)
+    with ctx.pmd_start(rg.ring) as m:
+        m.post(P)
+        m.post(P)
+        m.wait()
+    check(*rg.read(), ro, fos, B, P)
+
+
+def test_pmd_imix(gpu_ctx_factory):
+    """IMIX slab + u32 offsets per slot."""
+    rules = fw1k()
+    rts = routes(20000)
+    ctx = gpu_ctx_factory(stages=S | F | L)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    ctx.set_route_lpm(cg.LpmTable(rts, 1 << 20, 1 << 16, False))
+    B, P = 20000, 3
+    slab, offs = cg.gen_imix(0x5EED0B30, B, rules, rts)
+    per = ((slab.nbytes + offs.nbytes + 4095) // 4096) * 4096
+    dp = ctx.alloc(per * P)
+    for s in range(P):
+        dp.upload(slab, s * per)
+        dp.upload(offs, s * per + slab.nbytes)
+    dr = ctx.alloc(B * P * 8)
+    df = ctx.alloc(B * P * 4)
+    dc = ctx.alloc(P * 4)
+    ring = cg.make_ring(dp, P, B, dr, per, offsets=dp.addr + slab.nbytes, offsets_slot_words=per // 4,
+                        fwd_idx=df, fwd_slot=B, fwd_count=dc)
+    with ctx.pmd_start(ring) as m:
+        m.post(P)
+        m.wait()
+    fw, rt = oracle_tables(rules, rts)
+    r1, f1, _ = orc.process(slab, B, offsets=offs, stages=S | F | L, fw=fw, route=rt)
+    res = dr.download(cg.RESULT_DT, B * P)
+    fwd = df.download(np.uint32, B * P)
+    cnt = dc.download(np.uint32, P)
+    for s in range(P):
+        assert np.array_equal(res[s * B:(s + 1) * B].view(np.uint8), r1.view(np.uint8))
+        assert int(cnt[s]) == len(f1) and np.array_equal(fwd[s * B:s * B + len(f1)], f1)
+
+
+def test_pmd_dir24_rule_counters(gpu_ctx_factory):
+    """FW and route stage both DIR-24-8 in HBM, per-rule hit counters (the
+    EXT kernel): counters equal the oracle's hits over every posted batch."""
+    rules = fw1k()
+    rts = routes()
+    ctx = gpu_ctx_factory(stages=S | F | L, flags=cg.CFG_FW_FORCE_DIR24 | cg.CFG_RULE_COUNTERS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    ctx.set_route_lpm(cg.LpmTable(rts, 1 << 20, 1 << 16, False))
+    B, P = 65536, 6
+    pk = cg.gen_trace(0x5EED0B40, B * P, rules, rts)
+    fw, rt = oracle_tables(rules, rts)
+    ro, fos = oracle_slots(pk, B, P, S | F | L, fw, rt)
+    rg = Ring(ctx, pk, B, P)
+    with ctx.pmd_start(rg.ring) as m:
+        m.post(P)
+        m.post(2)
+        m.wait()
+    check(*rg.read(), ro, fos, B, P)
+    hits = ctx.rule_counters()
+    per_slot = [int(np.sum((ro["flags"][s * B:(s + 1) * B] & cg.FLAG_FW_HIT) != 0)) for s in range(P)]
+    assert int(hits.sum()) == sum(per_slot) + per_slot[0] + per_slot[1]
+
+
+def test_pmd_demux_port_stats(gpu_ctx_factory):
+    """One ordered forward list per vport and per-port counters."""
+    rules = fw1k()
+    K = 5
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_DEMUX_PORTS | cg.CFG_PORT_STATS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    B, P = 65536, 4
+    pk = cg.gen_trace(0x5EED0B50, B * P, rules)
+    fw, _ = oracle_tables(rules)
+    ro, fos = oracle_slots(pk, B, P, S | F, fw)
+    rg = Ring(ctx, pk, B, P, lists=K)
+    with ctx.pmd_start(rg.ring) as m:
+        m.post(P)
+        m.wait()
+    res, fwd, cnt = rg.read()
+    assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
+    for s in range(P):
+        port = ro["port"][s * B:(s + 1) * B]
+        for q in range(K):
+            want = fos[s][port[fos[s]] == q]
+            c = int(cnt[s * K + q])
+            assert np.array_equal(fwd[s * B * K + q * B: s * B * K + q * B + c], want), f"slot {s} port {q}"
+    ps = ctx.port_stats()
+    for q in range(K):
+        assert ps[q]["rx_packets"] == int(np.sum(ro["port"] == q))
+
+
+def test_pmd_idle_exit_relaunch_and_restart(gpu_ctx_factory, monkeypatch):
+    """The kernel leaves after an idle spell ($COP_PMD_IDLE_MS) and the next
+    post relaunches it; tables cannot change under it (-EBUSY); after stop,
+    one-shot launches and a second poll-mode kernel work on the context."""
+    monkeypatch.setenv("COP_PMD_IDLE_MS", "50")
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F)
+    tab = cg.LpmTable(rules, 1024, 24, True)
+    ctx.set_fw_table(tab)
+    B, P = 65536, 4
+    pk = cg.gen_trace(0x5EED0B60, B * P, rules)
+    fw, _ = oracle_tables(rules)
+    ro, fos = oracle_slots(pk, B, P, S | F, fw)
+    rg = Ring(ctx, pk, B, P)
+    m = ctx.pmd_start(rg.ring)
+    with pytest.raises(cg.CopError):
+        ctx.set_fw_table(tab)
+    m.post(2)
+    m.wait()
+    time.sleep(0.5)
+    assert m.info()["state"] == 2            # left idle
+    m.post(P)
+    m.wait()
+    assert m.info()["launches"] == 2
+    check(*rg.read(), ro, fos, B, P)
+    m.stop()
+    ctx.set_fw_table(tab)                    # allowed again
+    rg.dr.fill(0xAB)
+    ctx.submit_ring(rg.ring, 0, P)
+    ctx.sync()
+    check(*rg.read(), ro, fos, B, P)
+    rg.dr.fill(0xAB)
+    with ctx.pmd_start(rg.ring) as m2:
+        m2.post(P)
+        m2.wait()
+    check(*rg.read(), ro, fos, B, P)
