@@ -476,11 +476,14 @@ struct Counts {
     uint32_t total = 0, notv4 = 0, fwd = 0, dropfw = 0, parse = 0, noport = 0, rhit = 0, rx = 0;
 };
 
+// rec_stage != nullptr: the records go to LDS (tile order) instead, and
+// copy_out_records writes them as 16-byte stores once the tile's barrier
+// has passed (the poll-mode kernel's write-through stores: wide stores)
 template <int PPT, bool WT>
 __device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base, int tid, const bool (&valid)[PPT],
                                               const uint32_t (&verdict)[PPT], const uint32_t (&flags)[PPT],
                                               const uint32_t (&port)[PPT], const uint32_t (&rnh)[PPT],
-                                              bool (&fwd)[PPT], Counts &c)
+                                              bool (&fwd)[PPT], Counts &c, uint32_t *rec_stage)
 {
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
@@ -489,7 +492,8 @@ __device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base,
             u32x2 rec;
             rec.x = verdict[k] | (flags[k] << 8) | (port[k] << 16);
             rec.y = rnh[k];
-            st_u32x2<WT>(rec, &((u32x2 *)B.results)[base + k * BLOCK + tid]);
+            if (rec_stage) *(u32x2 *)&rec_stage[2 * (k * BLOCK + tid)] = rec;
+            else st_u32x2<WT>(rec, &((u32x2 *)B.results)[base + k * BLOCK + tid]);
             c.rx++;
             c.fwd += verdict[k] == COPK_FORWARD;
             c.dropfw += verdict[k] == COPK_DROP_FW;
@@ -498,6 +502,22 @@ __device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base,
             c.rhit += flags[k] & COPK_FLAG_ROUTE_HIT;
         }
     }
+}
+
+// Copy a tile's staged records (m = valid packets of the tile, 8 B each,
+// LDS in tile order) to results[base ..]: 16-byte stores (two records), an
+// 8-byte store for an odd last one. All BLOCK threads; results 16-byte
+// aligned at even packet indices (base is a multiple of 256).
+template <bool WT>
+__device__ __forceinline__ void copy_out_records(void *results, uint32_t base, uint32_t m, const uint32_t *stage,
+                                                 int tid)
+{
+    uint32_t *r = (uint32_t *)results + 2 * (size_t)base;
+    for (uint32_t c = (uint32_t)tid; c < m / 2; c += BLOCK) {
+        const u32x4 v = *(const u32x4 *)&stage[4 * c];
+        st_u32x4<WT>(v, r, 4 * (long)c);
+    }
+    if ((m & 1u) && tid == 0) st_u32x2<WT>(*(const u32x2 *)&stage[2 * (m - 1)], (u32x2 *)&r[2 * (m - 1)]);
 }
 
 // Copy a tile's forward list (agg indices staged in LDS, in order) to

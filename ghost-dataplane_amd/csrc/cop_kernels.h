@@ -88,6 +88,7 @@ struct CopKParams {
     // LDS carve (u32 words)
     uint32_t lds_fw_off, lds_lpm_off, lds_misc_off;
     uint32_t lds_stage_off;   // one-shot kernel: the tile's forward list staged in LDS (0: none)
+    uint32_t lds_rec_off;     // poll-mode kernel: the tile's records staged in LDS (0: none)
     // ordering / accounting state
     unsigned long long *tickets;   // one counter per batch, one 128-byte line each (zero at launch)
     unsigned long long *zero_tickets;  // the lane's other ticket buffer: zeroed by this launch

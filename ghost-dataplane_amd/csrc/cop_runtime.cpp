@@ -711,7 +711,8 @@ static Plan plan_launch(const cop_ctx *c, uint64_t total, bool imix, uint32_t mi
 // (LDS interval form or HBM DIR-24-8, falling back to DIR-24-8 when LDS
 // would overflow), table pointers, the LDS carve, counters and options.
 // p.stages, p.compact and p.demux are set by the caller.
-static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int *lpm_mode_out, uint32_t *lds_out)
+static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int *lpm_mode_out, uint32_t *lds_out,
+                       bool stage_records = false)
 {
     const uint32_t stages = p.stages;
     int fw_mode = pick_mode(c, c->fw, (stages & COP_STAGE_FW) != 0, (c->cfg.flags & COP_CFG_FW_FORCE_DIR24) != 0);
@@ -728,7 +729,8 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     const bool stage_list = p.compact && !p.demux && c->stage_lists;
     auto lds_need = [&](int fwm, int lpmm) {
         return (256u + c->rt_nleaf * 128u + (fwm == COPK_TBL_IVT ? 2u * c->fw.m : 0u) +
-                (lpmm == COPK_TBL_IVT ? 2u * c->lpm.m : 0u) + misc_words + (stage_list ? COPK_BLOCK * ppt : 0u)) *
+                (lpmm == COPK_TBL_IVT ? 2u * c->lpm.m : 0u) + misc_words + (stage_list ? COPK_BLOCK * ppt : 0u) +
+                (stage_records ? 2u * COPK_BLOCK * ppt : 0u)) *
                    4u +
                c->lds_pad;
     };
@@ -761,6 +763,11 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     if (stage_list) {
         p.lds_stage_off = off;   // the tile's forward list, written out in 16-byte stores
         off += COPK_BLOCK * ppt;
+    }
+    p.lds_rec_off = 0;
+    if (stage_records) {
+        p.lds_rec_off = off;     // the tile's records, written out in 16-byte stores
+        off += 2 * COPK_BLOCK * ppt;
     }
     p.counters = c->counters;
     p.rule_hits = (fw_mode != COPK_TBL_OFF && c->n_rule_ctr) ? c->counters + RULE_OFF : nullptr;
@@ -1679,7 +1686,11 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         goto fail;           \
     } while (0)
     {
-        if ((rc = fill_launch(c, p, ppt, &m->fw_mode, &m->lpm_mode, &m->lds_bytes))) goto fail;
+        // records as 16-byte write-through stores from LDS: every slot's
+        // records 16-byte aligned
+        const bool stage_rec = !getenv("COP_PMD_NO_REC_STAGE") && ((uintptr_t)r->results & 15) == 0 &&
+                               (r->results_slot & 1) == 0;
+        if ((rc = fill_launch(c, p, ppt, &m->fw_mode, &m->lpm_mode, &m->lds_bytes, stage_rec))) goto fail;
         p.dbg = 0;   // no ablations in the persistent kernel
         p.stamps = nullptr;
         const bool stamps = getenv("COP_PMD_STAMPS") != nullptr;

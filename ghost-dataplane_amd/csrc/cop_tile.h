@@ -162,9 +162,17 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
     bool fwd[PPT];
 #pragma unroll
     for (int k = 0; k < PPT; k++) fwd[k] = valid[k] && verdict[k] == COPK_FORWARD;
-    auto records = [&] { store_records<PPT, WT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn); };
+    uint32_t *rec_stage = (WT && p.lds_rec_off) ? lc.s_misc - p.lds_misc_off + p.lds_rec_off : nullptr;
+    auto records = [&] {
+        store_records<PPT, WT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn, rec_stage);
+    };
     if (p.compact) compact_tile<PPT, WT>(lk, o, B, look_off, j, base, fwd, port, lc.cl, tid, lane, wave, records);
     else records();
+    if (rec_stage) {
+        // compact_tile's second barrier (or this one) orders the staged records
+        if (!p.compact) lds_barrier();
+        copy_out_records<WT>(B.results, base, B.n > base ? min(B.n - base, (uint32_t)TILE) : 0u, rec_stage, tid);
+    }
     STAMP(5);
 
     // ---- counters (one flush per workgroup) ----
