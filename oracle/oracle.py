@@ -52,6 +52,17 @@ def lib():
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
             "orc_coprocessor_bench": (c_double, [c_void_p, c_uint64, c_void_p, c_double, c_int, c_int,
                                                  POINTER(c_uint64), POINTER(c_double)]),
+            # dpdk_lpm_v1604.c: the literal rules_tbl / rule_info restatement
+            "dl_lpm_create": (c_void_p, [c_uint32, c_uint32]),
+            "dl_lpm_free": (None, [c_void_p]),
+            "dl_lpm_add": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32]),
+            "dl_lpm_lookup_batch": (None, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
+            "dl_lpm_setup": (ctypes.c_int64, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_int,
+                                              POINTER(ctypes.c_int32), c_void_p]),
+            "dl_lpm_n_rules": (c_uint32, [c_void_p]),
+            "dl_lpm_tbl8_used": (c_uint32, [c_void_p]),
+            "dl_lpm_rule_info": (None, [c_void_p, c_void_p, c_void_p]),
+            "dl_lpm_rules": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -63,6 +74,69 @@ def lib():
 
 def _p(a):
     return a.ctypes.data_as(c_void_p) if a is not None else None
+
+
+class DpdkLpm:
+    """The literal restatement of DPDK 17.11 rte_lpm's v1604 add path
+    (oracle/dpdk_lpm_v1604.c): rules_tbl grouped by depth with
+    rule_info[depth-1] = {used_rules, first_rule}, rule_add_v1604 /
+    rule_delete_v1604, tbl8_alloc_v1604, add_depth_small/big_v1604."""
+
+    def __init__(self, max_rules=1024, number_tbl8s=24):
+        self.h = lib().dl_lpm_create(max_rules, number_tbl8s)
+        if not self.h:
+            raise MemoryError("dl_lpm_create")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().dl_lpm_free(self.h)
+            self.h = None
+
+    def add(self, ip, depth, nh) -> int:
+        return lib().dl_lpm_add(self.h, ip & 0xFFFFFFFF, depth, nh & 0xFFFFFFFF)
+
+    def setup(self, ip, depth, nh, stop_at_error=True):
+        """lpm_setup's loop: (index of the first failed add or -1, its errno,
+        every add's return code; -9999 = never presented)."""
+        ip = np.ascontiguousarray(ip, dtype=np.uint32)
+        depth = np.ascontiguousarray(depth, dtype=np.uint8)
+        nh = np.ascontiguousarray(nh, dtype=np.uint32)
+        rc = np.zeros(len(ip), dtype=np.int32)
+        err = ctypes.c_int32(0)
+        first = lib().dl_lpm_setup(self.h, _p(ip), _p(depth), _p(nh), len(ip), 1 if stop_at_error else 0,
+                                   byref(err), _p(rc))
+        return int(first), err.value, rc
+
+    def lookup(self, ips: np.ndarray):
+        ips = np.ascontiguousarray(ips, dtype=np.uint32)
+        nh = np.zeros(len(ips), dtype=np.uint32)
+        hit = np.zeros(len(ips), dtype=np.uint8)
+        lib().dl_lpm_lookup_batch(self.h, _p(ips), len(ips), _p(nh), _p(hit))
+        return nh, hit
+
+    @property
+    def n_rules(self):
+        return lib().dl_lpm_n_rules(self.h)
+
+    @property
+    def tbl8_used(self):
+        return lib().dl_lpm_tbl8_used(self.h)
+
+    def rule_info(self):
+        used = np.zeros(32, dtype=np.uint32)
+        first = np.zeros(32, dtype=np.uint32)
+        lib().dl_lpm_rule_info(self.h, _p(used), _p(first))
+        return used, first
+
+    def rules(self):
+        """(ip, depth, nh) in rules_tbl order: grouped by depth."""
+        n = self.n_rules
+        ip = np.zeros(n, dtype=np.uint32)
+        d = np.zeros(n, dtype=np.uint8)
+        nh = np.zeros(n, dtype=np.uint32)
+        k = lib().dl_lpm_rules(self.h, _p(ip), _p(d), _p(nh), n)
+        assert k == n
+        return ip, d, nh
 
 
 class OracleLpm:

@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
-"""Generate the committed golden fixtures (tests/golden/*.npz).
+"""Generate the committed fixtures (tests/golden/*.npz).
 
-The reference ships no golden vectors for this path and cannot
-be built here (DPDK absent), so these fixtures are produced by the oracle's
-C restatement (oracle/cop_oracle.c) on small seeded inputs, and pinned
-against the reference's own fixture (reference_rules.json: both rules
-accept, so every IPv4 packet that reaches the coprocessor is forwarded).
+Only g1 holds a REFERENCE fixture: the reference's own rules.json
+(reference_rules.json: both rules accept, so every IPv4 packet that reaches
+the coprocessor is forwarded). g2-g6 are ORACLE REGRESSION VECTORS, not
+reference goldens: the reference ships no vectors for this path (SURVEY.md
+§4) and cannot be built here (DPDK absent), so they are produced by the
+oracle's C restatement (oracle/cop_oracle.c) on small seeded inputs. They
+pin the product and the oracle against later changes of either; parity with
+the reference's own outputs stays unpinned beyond g1.
 Each .npz holds inputs (rules, packets, routing table, stage mask) and the
 expected outputs (8-byte result records, ordered forward list, counters).
 

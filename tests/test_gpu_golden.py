@@ -1,6 +1,7 @@
-"""GPU pipeline (through the C ABI) against the committed golden fixtures
-(tests/golden/*.npz, produced by the oracle; g1 is the reference's own
-rules.json fixture)."""
+"""GPU pipeline (through the C ABI) against the committed fixtures
+(tests/golden/*.npz): g1 is the reference's own rules.json fixture; g2-g6
+are oracle regression vectors (produced by oracle/cop_oracle.c, not by the
+reference: see make_golden.py)."""
 import glob
 import os
 
