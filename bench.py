@@ -43,6 +43,9 @@ import copgpu as cg  # noqa: E402
 
 METRIC = "Mpkt/s device-resident coprocessor NF pipeline (64B pkts); HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# counter words ahead of the per-rule ones in the RCCL reduction: the
+# COP_COUNTER_SHARDS x 16 counter shards, then as many port-stat shards
+SHARD_AND_PORT_WORDS = 2 * 16 * cg.COUNTER_SHARDS
 
 S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
 # config_id follows BASELINE.json configs[] (1-based); seeds per SURVEY.md §8d
@@ -240,14 +243,10 @@ def main():
     def run_steps(first, count):
         """Steps first .. first+count-1: batch s sits in ring slot s % P."""
         if pmd is not None:
-            # the poll-mode kernel's batch sequence is the step sequence;
-            # posts of at most a quarter of the ring keep it from draining
-            # (a post waits only for the slots it reuses)
-            s = 0
-            while s < count:
-                k = min(max(1, P // 4), count - s)
-                pmd.post(k)
-                s += k
+            # the poll-mode kernel's batch sequence is the step sequence:
+            # one call posts them (a quarter ring per post, so the ring never
+            # drains) and waits for the last
+            pmd.run(count)
             return
         s = first
         while s < first + count:
@@ -257,8 +256,9 @@ def main():
 
     def sync_all():
         if pmd is not None:
-            pmd.wait()
-        ctx.sync()
+            pmd.wait()      # (run_steps has waited already; the lanes hold no work)
+        else:
+            ctx.sync()
 
     # ---- warmup, then exactly K timed steps, `repeats` times; the value is
     # the median run (median of 5 runs) ----
@@ -305,14 +305,12 @@ def main():
         longs = []
         for _ in range(3):
             t0 = time.perf_counter()
-            pmd.post(n_long)
-            pmd.wait()
+            pmd.run(n_long)
             longs.append(time.perf_counter() - t0)
         lat = []
         for _ in range(50):
             t0 = time.perf_counter()
-            pmd.post(1)
-            pmd.wait()
+            pmd.run(1)
             lat.append((time.perf_counter() - t0) * 1e6)
         info = pmd.info()
         t_long = float(np.median(longs))
@@ -331,10 +329,10 @@ def main():
         ctx.coll_reduce_counters(reset=False, with_rules=False)
         r_ms = (time.perf_counter() - r0) * 1e3
         n_rules = len(ctx.rule_counters())
-        reduce_info = {"rccl_allreduce_u64_words": 1024 + n_rules, "ms": round(group.max(r_ms), 3),
+        reduce_info = {"rccl_allreduce_u64_words": SHARD_AND_PORT_WORDS + n_rules, "ms": round(group.max(r_ms), 3),
                        "pkts_reduced": int(red_tot["rx"]), "expected_pkts": world * (args.warmup + args.steps) * B}
         assert red_tot["rx"] == world * (args.warmup + args.steps) * B, (red_tot, world, args.steps)
-        log(f"[rank {rank}] rccl counter all-reduce of {1024 + n_rules} u64: {r_ms:.3f} ms")
+        log(f"[rank {rank}] rccl counter all-reduce of {SHARD_AND_PORT_WORDS + n_rules} u64: {r_ms:.3f} ms")
 
     # ---- kernel duration per launch (HIP events on the context stream) ----
     run_steps(0, Lb)   # untimed: loads the one-shot kernel's code object (first launch)

@@ -21,6 +21,7 @@ LIB_PATH = os.path.join(HERE, "libcopgpu.so")
 STAGE_PARSE, STAGE_FW, STAGE_LPM = 0x1, 0x2, 0x4
 FORWARD, DROP_FW, DROP_PARSE, DROP_NOT_IPV4, DROP_NO_PORT = 0, 1, 2, 3, 4
 FLAG_ROUTE_HIT, FLAG_FW_HIT = 0x1, 0x2
+COUNTER_SHARDS = 256   # COP_COUNTER_SHARDS
 LPM_STOP_AT_FIRST_ERROR = 0x1
 CFG_FW_FORCE_DIR24, CFG_LPM_FORCE_DIR24, CFG_NO_COMPACT, CFG_RULE_COUNTERS = 0x1, 0x2, 0x4, 0x8
 CFG_DEMUX_PORTS, CFG_PORT_STATS = 0x10, 0x20
@@ -129,6 +130,7 @@ SIGNATURES = {
     "cop_pmd_post": (c_int, [c_void_p, c_uint32]),
     "cop_pmd_wait": (c_int, [c_void_p, c_uint64]),
     "cop_pmd_posted": (c_uint64, [c_void_p]),
+    "cop_pmd_run": (c_int, [c_void_p, c_uint64]),
     "cop_pmd_info": (c_int, [c_void_p, POINTER(PmdInfo)]),
     "cop_pmd_stop": (c_int, [c_void_p]),
     "cop_poll": (c_int, [c_void_p]),
@@ -600,6 +602,10 @@ class Pmd:
         if seq is None:
             seq = self.posted
         _check(lib().cop_pmd_wait(self.handle, seq), self.ctx, "pmd_wait")
+
+    def run(self, count: int):
+        """Post `count` batches and wait for all of them (one C call)."""
+        _check(lib().cop_pmd_run(self.handle, count), self.ctx, "pmd_run")
 
     @property
     def posted(self) -> int:

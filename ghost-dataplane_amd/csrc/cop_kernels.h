@@ -9,7 +9,7 @@
 #define COPK_BLOCK 256
 #define COPK_MAXB 32
 #define COPK_MAX_LAUNCH_BATCHES 1024   /* ring launches; ticket lines per lane buffer */
-#define COPK_COUNTER_SHARDS 64   /* 16 u64 per shard (128 B) */
+#define COPK_COUNTER_SHARDS 256  /* 16 u64 per shard (128 B) */
 static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_LDS_MISC_WORDS 80       /* counts, tile, prefix, counter reduction */
 #define COPK_LDS_MISC_EXT_WORDS 408  /* + per-port counts/prefixes (demux, port stats) */
@@ -112,7 +112,7 @@ struct CopKPmd {
     const uint32_t *h_stop;              // host-mapped: non-zero = leave once idle
     unsigned long long *h_done;          // host-mapped: [slot] = sequence + 1 of its last completed batch
     uint32_t *h_state;                   // host-mapped: [0] exit reason (COPK_PMD_*), [1] census
-    unsigned long long *d_posted;        // device relay of *h_posted
+    unsigned long long *d_posted;        // device relays of *h_posted: COPK_PMD_RELAYS copies, 128 B apart
     uint32_t *d_ctl;                     // device: [0] exit (COPK_PMD_*), [1] census, [2] look-back timeout
     unsigned long long *slot_tiles;      // per ring slot: tiles completed (monotonic)
     unsigned long long *stamps;          // diagnostic: s_memrealtime per worker phase (COP_PMD_STAMPS) or null
@@ -121,6 +121,7 @@ struct CopKPmd {
     uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
     uint32_t idle_ticks;                 // s_memrealtime ticks (100 MHz) without a post before leaving
 };
+#define COPK_PMD_RELAYS 8
 #define COPK_PMD_RUNNING 0u
 #define COPK_PMD_STOPPED 1u   /* the host asked (cop_pmd_stop) */
 #define COPK_PMD_IDLE 2u      /* no post for idle_ticks: left; the next post relaunches */

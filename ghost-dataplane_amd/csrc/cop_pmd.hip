@@ -62,16 +62,20 @@ __device__ __forceinline__ void pmd_leave(const CopKPmd &P, uint32_t why)
 // (no new post for idle_ticks) into the exit word.
 __device__ unsigned long long wait_posted(const CopKPmd &P, unsigned long long b, bool leader)
 {
+    // this worker's copy of the relay (one 128-byte line per XCD-sized
+    // group of workers): a thousand pollers on one line would hammer one
+    // memory channel while other workers stream
+    unsigned long long *relay = P.d_posted + (blockIdx.x % COPK_PMD_RELAYS) * 16;
     unsigned long long seen = 0, t_seen = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        unsigned long long hp = __hip_atomic_load(P.d_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t spins = 0;; spins++) {
+        unsigned long long hp = __hip_atomic_load(relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (hp > b) return hp;
         if (ld_agent(&P.d_ctl[0])) return 0;
         if (leader) {
             const unsigned long long h = __hip_atomic_load(P.h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
             if (h > hp) {
-                atomicMax(P.d_posted, h);
+                for (int r = 0; r < COPK_PMD_RELAYS; r++) atomicMax(P.d_posted + r * 16, h);
                 if (P.stamps) {   // diagnostic: when each doorbell value was relayed
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2], h);
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2 + 1], now);
@@ -85,6 +89,9 @@ __device__ unsigned long long wait_posted(const CopKPmd &P, unsigned long long b
             if (ld_agent(&P.d_ctl[2])) pmd_leave(P, COPK_PMD_ABORT);   // a look-back timed out
             else if (__hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) pmd_leave(P, COPK_PMD_STOPPED);
             else if (now - t_seen > P.idle_ticks) pmd_leave(P, COPK_PMD_IDLE);
+        } else {
+            // back off to ~0.5 us between polls while nothing comes
+            for (uint32_t k = spins < 16 ? 0u : 3u; k; k--) __builtin_amdgcn_s_sleep(4);
         }
         __builtin_amdgcn_s_sleep(2);
     }

@@ -1541,13 +1541,17 @@ struct cop_pmd {
     bool live = false;                      // a launch may still be running
 };
 
+// device words: [8] d_ctl, [256 + 128 r] relay r, then the slot tile counts
+constexpr size_t PMD_RELAY_OFF = 256;
+constexpr size_t PMD_CTL_BYTES = PMD_RELAY_OFF + 128 * COPK_PMD_RELAYS;
+
 static int pmd_launch(cop_pmd *m, uint64_t seq0)
 {
     cop_ctx *c = m->c;
     HIPCHK(c, hipSetDevice(c->device));
     // device control words (d_posted, d_ctl) restart at 0; the slot tile
     // counts carry over (every served batch completed: multiples of tpb)
-    HIPCHK(c, hipMemsetAsync(m->dev, 0, 64, m->s));
+    HIPCHK(c, hipMemsetAsync(m->dev, 0, PMD_CTL_BYTES, m->s));
     m->h_state[0] = 0;
     m->h_state[1] = 0;
     *m->h_stop = 0;
@@ -1693,8 +1697,8 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         if ((rc = fill_launch(c, p, ppt, &m->fw_mode, &m->lpm_mode, &m->lds_bytes, stage_rec))) goto fail;
         p.dbg = 0;   // no ablations in the persistent kernel
         p.stamps = nullptr;
-        const bool stamps = getenv("COP_PMD_STAMPS") != nullptr;
-        if (stamps) {   // diagnostic: the tile body's phase stamps too (EXT kernel)
+        const char *stamps_env = getenv("COP_PMD_STAMPS");
+        if (stamps_env && atoi(stamps_env) >= 2) {   // diagnostic: the tile body's phase stamps too (EXT kernel)
             if (hipMalloc(&p.stamps, (size_t)c->ncu * 8 * 8 * 8) != hipSuccess)
                 PMD_FAIL(set_err(c, -ENOMEM, "pmd: stamps"));
             p.dbg = 8;
@@ -1708,7 +1712,7 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         // pipeline kernels' ~106 SGPRs, below what the API may answer; the
         // start-up census confirms, else one fewer per CU is tried
         occ = std::min(occ, 6);
-        if (getenv("COP_PMD_STAMPS")) occ = std::min(occ, 4);   // the EXT diagnostic kernel holds more registers
+        if (p.dbg) occ = std::min(occ, 4);   // the EXT diagnostic kernel holds more registers
         if (const char *env = getenv("COP_PMD_PER_CU")) occ = std::min(occ, std::max(1, atoi(env)));
         m->per_cu = (uint32_t)occ;
         pmd_size(m);
@@ -1730,8 +1734,8 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         m->P.h_stop = (const uint32_t *)((uint8_t *)dctl + 8);
         m->P.h_state = (uint32_t *)((uint8_t *)dctl + 16);
         m->P.h_done = (unsigned long long *)((uint8_t *)dctl + 64);
-        // device words: [0] relay, [8] ctl, [64] slot tile counts, then look-back
-        const size_t look_off = (64 + (size_t)m->n_slots * 8 + 255) & ~(size_t)255;
+        // device words: control and relays, slot tile counts, then look-back
+        const size_t look_off = (PMD_CTL_BYTES + (size_t)m->n_slots * 8 + 255) & ~(size_t)255;
         const size_t look_words = (size_t)m->n_slots * m->tpb * (p.demux ? p.demux : 1u);
         m->dev_bytes = look_off + look_words * 8;
         if (getenv("COP_PMD_STAMPS")) {   // diagnostic phase stamps (cop_debug_pmd_stamps)
@@ -1744,9 +1748,9 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         if (hipStreamCreateWithFlags(&m->s, hipStreamNonBlocking) != hipSuccess)
             PMD_FAIL(set_err(c, -EIO, "pmd: stream"));
         if (memset_sync(m->dev, 0, m->dev_bytes, m->s) != hipSuccess) PMD_FAIL(set_err(c, -EIO, "pmd: memset"));
-        m->P.d_posted = (unsigned long long *)m->dev;
+        m->P.d_posted = (unsigned long long *)(m->dev + PMD_RELAY_OFF);
         m->P.d_ctl = (uint32_t *)(m->dev + 8);
-        m->P.slot_tiles = (unsigned long long *)(m->dev + 64);
+        m->P.slot_tiles = (unsigned long long *)(m->dev + PMD_CTL_BYTES);
         p.look = (unsigned long long *)(m->dev + look_off);
         p.err = nullptr;   // the look-back reports through d_ctl[2] (LookCtx)
         p.epoch = 0;
@@ -1817,6 +1821,18 @@ int cop_pmd_wait(cop_pmd *m, uint64_t seq)
 }
 
 uint64_t cop_pmd_posted(const cop_pmd *m) { return m ? m->posted : 0; }
+
+int cop_pmd_run(cop_pmd *m, uint64_t count)
+{
+    if (!m) return -EINVAL;
+    const uint32_t chunk = std::max(1u, m->n_slots / 4);   // a quarter ring per post: the ring never drains
+    for (uint64_t done = 0; done < count;) {
+        const uint32_t k = (uint32_t)std::min<uint64_t>(chunk, count - done);
+        if (int rc = cop_pmd_post(m, k)) return rc;
+        done += k;
+    }
+    return cop_pmd_wait(m, m->posted);
+}
 
 int cop_pmd_info(const cop_pmd *m, cop_pmd_info_t *out)
 {

@@ -361,6 +361,9 @@ int cop_pmd_post(cop_pmd *pmd, uint32_t count);
  * kernels. 0, -ETIMEDOUT (30 s) or -EIO (the kernel aborted). */
 int cop_pmd_wait(cop_pmd *pmd, uint64_t seq);
 uint64_t cop_pmd_posted(const cop_pmd *pmd);
+/* Post `count` batches (in posts of a quarter ring, so it never drains) and
+ * wait for all of them: one synchronous burst. 0 or -errno. */
+int cop_pmd_run(cop_pmd *pmd, uint64_t count);
 typedef struct cop_pmd_info_t {
     uint32_t workers;          /* worker workgroups (all co-resident) */
     uint32_t workers_per_cu;
@@ -394,7 +397,7 @@ typedef struct cop_counters {
     uint64_t _rsvd[7];
 } cop_counters;
 #define COP_N_COUNTERS 16
-#define COP_COUNTER_SHARDS 64
+#define COP_COUNTER_SHARDS 256
 
 int  cop_counters_read(cop_ctx *ctx, cop_counters *out, int reset);
 /* Device address of the COP_COUNTER_SHARDS x COP_N_COUNTERS u64 counter

@@ -16,7 +16,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ghost-dataplane_amd"))
-os.environ["COP_PMD_STAMPS"] = "1"
+os.environ.setdefault("COP_PMD_STAMPS", "1")   # 1: tile stamps (production kernel); 2: + body phases (EXT kernel)
 import copgpu as cg  # noqa: E402
 
 
@@ -67,13 +67,19 @@ def main():
         body = mine[:, 2] - mine[:, 1]
         drain = mine[:, 3] - mine[:, 2]
         end = mine[:, 3] - t_relay
-        ts = buf[G * 8 + 128:G * 16 + 128].reshape(G, 8).astype(np.int64)
-        sel = np.isin(st[:, 4], list(last_batches))
-        tb = ts[sel]
-        ph = {"seen->pass1 (loads+P+lookups)": tb[:, 2] - mine[:, 1], "pass2": tb[:, 3] - tb[:, 2],
-              "compaction+records": tb[:, 5] - tb[:, 3], "counters": tb[:, 6] - tb[:, 5]}
-        print("   body phases (median/max us): " + "; ".join(f"{k2} {us(np.median(v)):.2f}/{us(v.max()):.2f}"
-                                                          for k2, v in ph.items()))
+        if n > G * 8 + 128:
+            ts = buf[G * 8 + 128:G * 16 + 128].reshape(G, 8).astype(np.int64)
+            sel = np.isin(st[:, 4], list(last_batches))
+            tb = ts[sel]
+            ph = {"seen->pass1 (loads+P+lookups)": tb[:, 2] - mine[:, 1], "pass2": tb[:, 3] - tb[:, 2],
+                  "compaction+records": tb[:, 5] - tb[:, 3], "counters": tb[:, 6] - tb[:, 5]}
+            print("   body phases (median/max us): " + "; ".join(f"{k2} {us(np.median(v)):.2f}/{us(v.max()):.2f}"
+                                                              for k2, v in ph.items()))
+        # when the tiles of the post finished, relative to the relay (us): quantiles
+        q = np.percentile(end, [10, 50, 90, 99, 100])
+        sq = np.percentile(seen, [10, 50, 90, 100])
+        print("   tile counted at (p10/p50/p90/p99/max us after relay): " + " ".join(f"{us(x):.1f}" for x in q)
+              + "; seen at (p10/p50/p90/max): " + " ".join(f"{us(x):.1f}" for x in sq))
         print(f"post {k:3d}: host post->done median {np.median(host):7.1f} us (min {min(host):.1f}); "
               f"{len(mine)} tiles; relay->seen min {us(seen.min()):.2f} med {us(np.median(seen)):.2f} "
               f"max {us(seen.max()):.2f}; body med {us(np.median(body)):.2f} max {us(body.max()):.2f}; "
