@@ -60,10 +60,20 @@ def main():
                 "dispatches": len(fv), "fetch_kib_raw": f, "write_kib_raw": w, "total_fetch_kib": sum(fv),
                 "read_bytes": f * 1024 * rf, "write_bytes": w * 1024 * wf,
                 "hbm_bytes_per_launch": f * 1024 * rf + w * 1024 * wf}
+    # the poll-mode kernel (one dispatch per launch, serving many batches):
+    # its total traffic, for bytes per packet over the packets it served
+    pmd = {}
+    for name in fb_:
+        if "cop_pmd" not in name:
+            continue
+        fv = [v for _, v in fb_[name]]
+        wv = [v for _, v in wb_.get(name, [])] or [0.0]
+        pmd[name] = {"dispatches": len(fv), "read_bytes_total": sum(fv) * 1024 * rf,
+                     "write_bytes_total": sum(wv) * 1024 * wf}
     main_k = max(res, key=lambda k: res[k]["total_fetch_kib"])
     doc = {"kernel": main_k, "hbm_bytes_per_launch": res[main_k]["hbm_bytes_per_launch"],
            "read_bytes_per_launch": res[main_k]["read_bytes"], "write_bytes_per_launch": res[main_k]["write_bytes"],
-           "calibration": cal, "kernels": res,
+           "calibration": cal, "kernels": res, "pmd": pmd,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; KiB per dispatch; "
                      "read factor calibrated on tools/membench kA (same access pattern, known bytes)"}
     json.dump(doc, open(out, "w"), indent=1)
