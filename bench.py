@@ -139,9 +139,10 @@ def main():
                     help="batches per kernel launch (ring submit, at most 1024; 0: the workload's default). The "
                          "~23 us per-launch ramp and tail cost 6 %% at 384 batches, 2.5 %% at 1024")
     ap.add_argument("--streams", type=int, default=1, help="launch lanes (concurrent streams)")
-    ap.add_argument("--engine", default="pmd", choices=("pmd", "launch"),
+    ap.add_argument("--engine", default="auto", choices=("auto", "pmd", "launch"),
                     help="pmd: the poll-mode kernel serves the batch ring (steps are posted to it); launch: one "
-                         "kernel launch per --per-launch steps")
+                         "kernel launch per --per-launch steps; auto: launch when per-rule counters are on (their "
+                         "binned counting runs after each launch), else pmd")
     ap.add_argument("--pool-mib", type=int, default=0,
                     help="distinct input bytes per GPU (0: max(400 MiB, one launch of batches))")
     ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the value is their median")
@@ -177,6 +178,8 @@ def main():
     else:
         fw_tab = cg.LpmTable(fw_rules, W["fw"], 1 << 20, False)
     rc_on = bool(W.get("rule_counters")) and not args.no_rule_counters
+    if args.engine == "auto":
+        args.engine = "launch" if rc_on else "pmd"
     if args.stages:
         W = dict(W, stages=args.stages)
     ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32, n_streams=args.streams,

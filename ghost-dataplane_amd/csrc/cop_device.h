@@ -404,6 +404,38 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
     }
 }
 
+// rte_lpm_lookup's tbl8 step for valid+extended tbl24 entries e[k]: a
+// direct group load, or (packed) the run block's header word, then the run's
+// entry (cop_kernels.h COPK_TBL_DIR). All PPT loads of a level are issued
+// before any is used.
+template <int PPT>
+__device__ __forceinline__ void tbl8_step(const uint32_t *tbl8, uint32_t packed, const uint32_t (&ip)[PPT],
+                                          uint32_t (&e)[PPT])
+{
+    bool ext[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) ext[k] = (e[k] & 0x03000000u) == 0x03000000u;
+    if (!packed) {
+#pragma unroll
+        for (int k = 0; k < PPT; k++)
+            if (ext[k]) e[k] = tbl8[((size_t)(e[k] & 0x00FFFFFFu) << 8) | (ip[k] & 0xFFu)];
+        return;
+    }
+    unsigned long long h[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++)
+        h[k] = ext[k] ? ((const unsigned long long *)(tbl8 + ((size_t)(e[k] & 0x00FFFFFFu) << 4)))[(ip[k] & 0xFFu) >> 5]
+                      : 0ull;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        if (ext[k]) {
+            const uint32_t bit = ip[k] & 31u;
+            const uint32_t rank = (uint32_t)(h[k] >> 32) + (uint32_t)__popc((uint32_t)h[k] & (0xFFFFFFFFu >> (31u - bit)));
+            e[k] = tbl8[((size_t)(e[k] & 0x00FFFFFFu) << 4) + 16u + rank - 1u];
+        }
+    }
+}
+
 // Pass 2: rte_lpm_lookup's tbl8 step for valid+extended entries, then the
 // verdicts of stage FW (firewall.c:183-210) and stage LPM. Packets that did
 // not reach the coprocessor (stage P drop) keep their verdict. Counts the
@@ -421,18 +453,8 @@ __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[
         flags[k] = 0;
         rnh[k] = 0;
     }
-    if (FW == COPK_TBL_DIR) {
-#pragma unroll
-        for (int k = 0; k < PPT; k++)
-            if ((fwe[k] & 0x03000000u) == 0x03000000u)
-                fwe[k] = p.fw_tbl8[((size_t)(fwe[k] & 0x00FFFFFFu) << 8) | (src[k] & 0xFFu)];
-    }
-    if (LPM == COPK_TBL_DIR) {
-#pragma unroll
-        for (int k = 0; k < PPT; k++)
-            if ((lpe[k] & 0x03000000u) == 0x03000000u)
-                lpe[k] = p.lpm_tbl8[((size_t)(lpe[k] & 0x00FFFFFFu) << 8) | (dst[k] & 0xFFu)];
-    }
+    if (FW == COPK_TBL_DIR) tbl8_step<PPT>(p.fw_tbl8, p.fw_tbl8_packed, src, fwe);
+    if (LPM == COPK_TBL_DIR) tbl8_step<PPT>(p.lpm_tbl8, p.lpm_tbl8_packed, dst, lpe);
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         if (!reached[k]) continue;

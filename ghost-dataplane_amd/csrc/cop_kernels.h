@@ -21,6 +21,13 @@ static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_TBL_OFF 0
 #define COPK_TBL_IVT 1  /* flattened intervals, binary search in LDS */
 #define COPK_TBL_DIR 2  /* DIR-24-8 image in HBM */
+/* Packed tbl8 form of a DIR-24-8 image: an extended tbl24 entry's payload is
+ * the offset (in 64-byte units) of its /24's run block instead of a group
+ * index. A block describes the group's 256 entries as runs of equal
+ * entries: 8 u64 header words h[w] = (runs starting before entry 32w) << 32
+ * | bitmap of the run starts among entries 32w..32w+31, then the runs'
+ * entries (u32). Entry i = value[prefix(w) + popcount(bits 0..i%32) - 1],
+ * w = i/32. Blocks are 64-byte aligned: 64 + 4*runs bytes, rounded up. */
 
 #define COPK_LAY_SLOTS 0      /* packet layouts of the one-shot kernel */
 #define COPK_LAY_IMIX 1
@@ -81,10 +88,12 @@ struct CopKParams {
     uint32_t fw_m;
     const uint32_t *fw_starts, *fw_vals;
     const uint32_t *fw_tbl24, *fw_tbl8;
+    uint32_t fw_tbl8_packed;  // tbl8 groups as packed run blocks (COPK_TBL8_PACKED form)
     // route LPM
     uint32_t lpm_m;
     const uint32_t *lpm_starts, *lpm_vals;
     const uint32_t *lpm_tbl24, *lpm_tbl8;
+    uint32_t lpm_tbl8_packed;
     // LDS carve (u32 words)
     uint32_t lds_fw_off, lds_lpm_off, lds_misc_off;
     uint32_t lds_stage_off;   // one-shot kernel: the tile's forward list staged in LDS (0: none)
@@ -101,7 +110,19 @@ struct CopKParams {
     uint32_t port_stats;               // > 0: per-port counters for ports < port_stats
     uint32_t *err;
     unsigned long long *stamps;   // diagnostic phase stamps (dbg bit 8)
+    // per-rule hit counters by binning (one-shot launches): each tile sorts
+    // its FW hits' rule ids by bucket (id >> COPK_HIT_SHIFT) in LDS and
+    // writes them to its region (runs padded to 4 ids with ~0u) plus the run
+    // offsets; cop_hit_count then counts bucket by bucket in LDS and adds
+    // the sums to rule_hits. hit_region == nullptr: one atomic per hit.
+    uint32_t *hit_region;     // [tile][hit_reg_words]
+    uint32_t *hit_off;        // [tile][hit_nb + 1]: run start of each bucket, then the end
+    uint32_t hit_nb;          // buckets (<= COPK_HIT_MAX_BUCKETS)
+    uint32_t hit_reg_words;   // tile * PPT*BLOCK + 4 * hit_nb
+    uint32_t lds_hit_off;     // LDS: cnt[nb] | cur[nb] | wsum[4] | off[nb+1] (padded to 4) | tmp[tile] | ids[hit_reg_words]
 };
+#define COPK_HIT_SHIFT 14            /* 16384 rules per bucket: the count kernel's LDS counters (64 KiB) */
+#define COPK_HIT_MAX_BUCKETS 256     /* 4M rules */
 
 // Poll-mode (persistent) kernel, cop_pmd.hip: n_work worker workgroups
 // serve a batch ring; every relay_stride-th one relays the host's doorbell.
@@ -138,6 +159,8 @@ hipError_t copk_pmd_occupancy(int fw_mode, int lpm_mode, int layout, int ppt, in
 // layout: COPK_LAY_*
 hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int layout, int ppt,
                        uint32_t grid, uint32_t lds_bytes, hipStream_t stream);
+// per-rule hit counters from the binned ids of n_tiles tiles (see hit_region)
+hipError_t copk_hit_count(const CopKParams *p, uint32_t n_tiles, uint32_t tile_pkts, hipStream_t stream);
 // dst[i] = src[i] (atomic load) or atomic exchange with 0 when reset
 hipError_t copk_snapshot(unsigned long long *src, uint32_t n_words, unsigned long long *dst, int reset,
                          hipStream_t stream);

@@ -49,7 +49,7 @@ using namespace copd;
 // EXT: the launch uses an optional feature (demux, port stats, per-rule
 // counters, $COP_DBG ablations); without, their code is compiled out.
 template <int FW, int LPM, int LAY, int PPT, bool EXT>
-__global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const CopKParams p)
+__global__ __launch_bounds__(BLOCK, EXT ? 4 : COPK_WAVES_PER_EU) void cop_pipeline(const CopKParams p)
 {
     const Opt o = EXT ? opt_all(p) : Opt{0u, 0u, 0u, nullptr};
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -74,6 +74,11 @@ __global__ __launch_bounds__(BLOCK, COPK_WAVES_PER_EU) void cop_pipeline(const C
     // lane (stream order puts that launch after this one completes) ----
     for (uint32_t line = g; line < p.zero_lines; line += gridDim.x)
         if (tid < 16) p.zero_tickets[line * 16 + tid] = 0ull;
+
+    // ---- per-rule hit binning: zero the tile's bucket counts (ordered
+    // before the first add by the barrier below or tile_body's) ----
+    if (EXT && p.hit_region)
+        for (uint32_t i = (uint32_t)tid; i < p.hit_nb; i += BLOCK) lds[p.lds_hit_off + i] = 0u;
 
     // ---- tile index inside the batch: this batch's ticket counter (or the
     // static order when no look-back runs: p.compact == 0) ----
@@ -143,6 +148,64 @@ extern "C" hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode
 }
 
 namespace {
+// Per-rule hit counters from binned ids (CopKParams::hit_region): workgroup
+// (q, s) counts bucket q's runs of the tiles in slice s into LDS counters,
+// then adds every non-zero counter to rule_hits (contiguous adds, one per
+// rule and slice). A lane's task is one chunk of up to HIT_CHUNK ids of one
+// tile's run (chunks per run: `chunks`), loaded four 16-byte loads at a time;
+// repeats of one id within a lane's loads are merged before the LDS add.
+constexpr uint32_t HIT_R = 1u << COPK_HIT_SHIFT;
+constexpr uint32_t HIT_CHUNK = 64;
+__global__ __launch_bounds__(256) void cop_hit_count(const CopKParams p, uint32_t n_tiles, uint32_t slices,
+                                                     uint32_t chunks)
+{
+    __shared__ uint32_t cnt[HIT_R];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t q = blockIdx.x / slices, s = blockIdx.x % slices, nb = p.hit_nb;
+    for (uint32_t i = tid; i < HIT_R; i += 256) cnt[i] = 0u;
+    __syncthreads();
+    const uint32_t per = (n_tiles + slices - 1) / slices;
+    const uint32_t t0 = s * per, t1 = min(n_tiles, t0 + per);
+    const uint32_t tasks = (t1 > t0 ? t1 - t0 : 0u) * chunks;
+    for (uint32_t k = tid; k < tasks; k += 256) {
+        const uint32_t t = t0 + k / chunks, c = k % chunks;
+        const uint32_t *ob = p.hit_off + (size_t)t * (nb + 1) + q;
+        const uint32_t a = ob[0] + c * HIT_CHUNK;
+        // the last chunk also takes whatever a run holds beyond chunks * HIT_CHUNK ids
+        const uint32_t end = c + 1 == chunks ? ob[1] : min(ob[1], a + HIT_CHUNK);
+        const uint32_t *reg = p.hit_region + (size_t)t * p.hit_reg_words;
+        uint32_t cur = 0xFFFFFFFFu, n = 0;
+        for (uint32_t i = a; i < end; i += 16) {
+            u32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                v[u] = i + 4 * u < end ? __builtin_nontemporal_load((const u32x4 *)&reg[i + 4 * u])
+                                       : u32x4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int cc = 0; cc < 4; cc++) {
+                    if (x[cc] == 0xFFFFFFFFu) continue;
+                    if (x[cc] == cur) {
+                        n++;
+                    } else {
+                        if (n) atomicAdd(&cnt[cur & (HIT_R - 1)], n);
+                        cur = x[cc];
+                        n = 1;
+                    }
+                }
+            }
+        }
+        if (n) atomicAdd(&cnt[cur & (HIT_R - 1)], n);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < HIT_R; i += 256)
+        if (cnt[i])
+            __hip_atomic_fetch_add(&p.rule_hits[(size_t)q * HIT_R + i], (unsigned long long)cnt[i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void cop_snapshot(unsigned long long *src, uint32_t n, unsigned long long *dst, int reset)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -151,6 +214,20 @@ __global__ void cop_snapshot(unsigned long long *src, uint32_t n, unsigned long 
                    : __hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 } // namespace
+
+extern "C" hipError_t copk_hit_count(const CopKParams *p, uint32_t n_tiles, uint32_t tile_pkts, hipStream_t stream)
+{
+    const uint32_t nb = max(1u, p->hit_nb);
+    // chunks per run: enough for a bucket's share of a whole tile
+    const uint32_t chunks = min(32u, max(1u, (tile_pkts / nb + HIT_CHUNK - 1) / HIT_CHUNK));
+    // about eight tasks per lane, at most ~two workgroups per CU (64 KiB of
+    // LDS each) over all buckets: every slice adds its non-zero counters to
+    // rule_hits, so more slices also mean more atomics
+    const uint32_t want = (uint32_t)(((uint64_t)n_tiles * chunks + 2047) / 2048);
+    const uint32_t slices = max(1u, min(want, 512u / nb));
+    hipLaunchKernelGGL(cop_hit_count, dim3(nb * slices), dim3(256), 0, stream, *p, n_tiles, slices, chunks);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t copk_snapshot(unsigned long long *src, uint32_t n_words, unsigned long long *dst, int reset,
                                     hipStream_t stream)

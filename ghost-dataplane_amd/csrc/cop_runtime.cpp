@@ -46,6 +46,8 @@ struct DevLpm {
     uint32_t *starts = nullptr, *vals = nullptr;
     uint32_t *tbl24 = nullptr, *tbl8 = nullptr;
     uint32_t n_ext = 0;
+    bool tbl8_packed = false;       // tbl8 as packed run blocks (COPK_TBL_DIR form note)
+    size_t tbl8_bytes = 0;
 };
 
 struct Lane {
@@ -57,6 +59,9 @@ struct Lane {
     int parity = 0;
     unsigned long long *look = nullptr;
     uint32_t look_cap = 0;
+    // per-rule hit binning buffers of this lane's launches (grown on demand)
+    uint32_t *hit_region = nullptr, *hit_off = nullptr;
+    size_t hit_region_cap = 0, hit_off_cap = 0;   // bytes
     uint32_t epoch = 0;
     hipEvent_t ev[TIMING_SLOTS][2];
     int ev_head = 0, ev_count = 0, ev_created = 0;
@@ -168,6 +173,7 @@ struct cop_ctx {
     int ppt_override = 0;      // $COP_PPT (1, 4, 8) for experiments; 0 = auto
     bool coalesced = true;     // one-shot kernel: coalesced header loads where eligible ($COP_LOADS=strided: off)
     bool stage_lists = true;   // one-shot kernel: forward lists staged in LDS ($COP_STAGE_LISTS=0: off)
+    bool hit_bins = true;      // per-rule hit counters by binning ($COP_HIT_BINS=0: one atomic per hit)
     uint32_t dbg = 0;          // $COP_DBG: timing-only kernel ablations
     uint32_t lds_pad = 0;      // $COP_LDS_PAD: extra LDS bytes per workgroup (occupancy experiments)
     unsigned long long *stamps = nullptr;   // dbg bit 8: per-workgroup phase stamps
@@ -320,6 +326,8 @@ void cop_destroy(cop_ctx *c)
         for (int q = 0; q < 2; q++)
             if (L.tickets[q]) (void)hipFree(L.tickets[q]);
         if (L.look) (void)hipFree(L.look);
+        if (L.hit_region) (void)hipFree(L.hit_region);
+        if (L.hit_off) (void)hipFree(L.hit_off);
         for (int i = 0; i < L.ev_created; i++) {
             (void)hipEventDestroy(L.ev[i][0]);
             (void)hipEventDestroy(L.ev[i][1]);
@@ -467,6 +475,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_ZC_MAX")) c->zc_max = (uint32_t)strtoul(e, nullptr, 0);
     if (const char *e = getenv("COP_LOADS")) c->coalesced = strcmp(e, "strided") != 0;
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
+    if (const char *e = getenv("COP_HIT_BINS")) c->hit_bins = atoi(e) != 0;
     if (const char *e = getenv("COP_STREAMS")) {
         int v = atoi(e);
         if (v >= 1 && v <= MAX_LANES) cfg.n_streams = (uint32_t)v;
@@ -536,6 +545,56 @@ static int sync_lanes(cop_ctx *c)
 
 // form: COP_FORM_RULE for the firewall (entries carry the matching rule id
 // and the drop bit), COP_FORM_NH for the route stage (entries carry nh)
+// Packed tbl8 groups ($COP_TBL8=packed|plain; default: packed once the
+// groups pass 16 MiB, i.e. large tables whose groups would crowd the
+// Infinity Cache). The form is described at COPK_TBL_DIR in cop_kernels.h.
+static bool tbl8_pack_wanted(uint32_t n_ext)
+{
+    if (const char *e = getenv("COP_TBL8")) {
+        if (!strcmp(e, "packed")) return n_ext > 0;
+        if (!strcmp(e, "plain")) return false;
+    }
+    return n_ext >= 16384;
+}
+
+// Rewrite a DIR-24-8 image's groups as packed run blocks: h8 becomes the
+// block array (u32 words, 64-byte blocks), and every extended tbl24 entry's
+// payload the offset of its block in 64-byte units.
+static void pack_tbl8(std::vector<uint32_t> &h24, std::vector<uint32_t> &h8)
+{
+    const size_t n_grp = h8.size() / 256;
+    std::vector<uint32_t> blk;
+    std::vector<uint32_t> off(n_grp);
+    blk.reserve(n_grp * 32);
+    for (size_t g = 0; g < n_grp; g++) {
+        const uint32_t *e = &h8[g * 256];
+        uint32_t words[8] = {0}, runs = 0, pre[8];
+        std::vector<uint32_t> vals;
+        for (uint32_t w = 0; w < 8; w++) {
+            pre[w] = runs;
+            for (uint32_t b = 0; b < 32; b++) {
+                const uint32_t i = w * 32 + b;
+                if (i == 0 || e[i] != e[i - 1]) {
+                    words[w] |= 1u << b;
+                    vals.push_back(e[i]);
+                    runs++;
+                }
+            }
+        }
+        off[g] = (uint32_t)(blk.size() / 16);
+        for (uint32_t w = 0; w < 8; w++) {
+            blk.push_back(words[w]);   // little-endian u64: low word = bitmap
+            blk.push_back(pre[w]);
+        }
+        blk.insert(blk.end(), vals.begin(), vals.end());
+        blk.resize((blk.size() + 15) & ~(size_t)15, 0u);
+    }
+    for (auto &x : h24)
+        if ((x & 0x03000000u) == 0x03000000u) x = (x & 0xFF000000u) | off[x & 0x00FFFFFFu];
+    if (blk.empty()) blk.resize(16, 0u);
+    h8.swap(blk);
+}
+
 static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt, int form)
 {
     if (int rc = sync_lanes(c)) return rc;
@@ -582,11 +641,15 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
     std::vector<uint32_t> h24((size_t)1 << 24);
     std::vector<uint32_t> h8((size_t)(n_ext ? n_ext : 1) * 256);
     cop_lpm_form_fill_dir24(tab, form, h24.data(), h8.data());
+    const bool packed = tbl8_pack_wanted(n_ext);
+    if (packed) pack_tbl8(h24, h8);
     HIPCHK(c, hipMalloc(&t.tbl24, h24.size() * 4));
     HIPCHK(c, hipMalloc(&t.tbl8, h8.size() * 4));
     HIPCHK(c, hipMemcpy(t.tbl24, h24.data(), h24.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(t.tbl8, h8.data(), h8.size() * 4, hipMemcpyHostToDevice));
     t.n_ext = n_ext;
+    t.tbl8_packed = packed;
+    t.tbl8_bytes = h8.size() * 4;
     t.loaded = true;
     HIPCHK(c, hipDeviceSynchronize());   // the copies have landed before any lane reads them
     return 0;
@@ -747,11 +810,13 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     p.fw_vals = c->fw.vals;
     p.fw_tbl24 = c->fw.tbl24;
     p.fw_tbl8 = c->fw.tbl8;
+    p.fw_tbl8_packed = c->fw.tbl8_packed ? 1u : 0u;
     p.lpm_m = lpm_mode == COPK_TBL_IVT ? c->lpm.m : 0;
     p.lpm_starts = c->lpm.starts;
     p.lpm_vals = c->lpm.vals;
     p.lpm_tbl24 = c->lpm.tbl24;
     p.lpm_tbl8 = c->lpm.tbl8;
+    p.lpm_tbl8_packed = c->lpm.tbl8_packed ? 1u : 0u;
     uint32_t off = 256 + c->rt_nleaf * 128;
     p.lds_fw_off = off;
     off += 2 * p.fw_m;
@@ -818,6 +883,43 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     p.err = c->d_err + 4 * (&L - c->lane);
     if ((c->dbg & 8u) && p.ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
     const uint32_t grid = p.ntiles;   // one tile per workgroup
+    // per-rule hit counters by binning: each tile sorts its hits' rule ids by
+    // bucket into its region, cop_hit_count adds them up after the launch
+    p.hit_region = nullptr;
+    p.hit_off = nullptr;
+    p.hit_nb = 0;
+    if (p.rule_hits && c->hit_bins) {
+        const uint32_t nb = (c->n_rule_ctr + (1u << COPK_HIT_SHIFT) - 1) >> COPK_HIT_SHIFT;
+        const uint32_t reg = COPK_BLOCK * (uint32_t)ppt + 4u * nb;
+        const uint32_t base = (lds_bytes / 4u + 3u) & ~3u;
+        const uint32_t words = ((3u * nb + 5u + 3u) & ~3u) + COPK_BLOCK * (uint32_t)ppt + reg;
+        if (nb >= 1 && nb <= COPK_HIT_MAX_BUCKETS && (base + words) * 4u <= 160u * 1024u) {
+            const size_t need_reg = (size_t)grid * reg * 4, need_off = (size_t)grid * (nb + 1) * 4;
+            if (need_reg > L.hit_region_cap || need_off > L.hit_off_cap) {
+                HIPCHK(c, hipStreamSynchronize(L.s));   // the lane's earlier launches are done with them
+                if (need_reg > L.hit_region_cap) {
+                    HIPCHK(c, hipFree(L.hit_region));
+                    L.hit_region = nullptr;
+                    L.hit_region_cap = 0;
+                    HIPCHK(c, hipMalloc(&L.hit_region, need_reg));
+                    L.hit_region_cap = need_reg;
+                }
+                if (need_off > L.hit_off_cap) {
+                    HIPCHK(c, hipFree(L.hit_off));
+                    L.hit_off = nullptr;
+                    L.hit_off_cap = 0;
+                    HIPCHK(c, hipMalloc(&L.hit_off, need_off));
+                    L.hit_off_cap = need_off;
+                }
+            }
+            p.hit_region = L.hit_region;
+            p.hit_off = L.hit_off;
+            p.hit_nb = nb;
+            p.hit_reg_words = reg;
+            p.lds_hit_off = base;
+            lds_bytes = (base + words) * 4u;
+        }
+    }
 
     if (c->timing) {
         if (L.ev_count == TIMING_SLOTS) harvest_one(c, L);
@@ -825,6 +927,8 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     }
     hipError_t e = copk_launch(&p, fw_mode, lpm_mode, pl.layout, ppt, grid, lds_bytes, L.s);
     if (e != hipSuccess) return set_err(c, -EIO, "launch: %s", hipGetErrorString(e));
+    if (p.hit_region && (e = copk_hit_count(&p, grid, COPK_BLOCK * (uint32_t)ppt, L.s)) != hipSuccess)
+        return set_err(c, -EIO, "hit count launch: %s", hipGetErrorString(e));
     L.dirty[q ^ 1] = 0;
     L.dirty[q] = (p.compact && !(c->dbg & 2u)) ? nb_used : 0;
     L.parity = q ^ 1;

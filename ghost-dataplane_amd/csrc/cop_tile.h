@@ -72,6 +72,110 @@ __device__ __forceinline__ void stage_tables(const CopKParams &p, const Tables &
     }
 }
 
+// Per-rule hit binning (CopKParams::hit_region): the LDS of the tile's sort
+struct HitLds {
+    uint32_t *cnt;    // [nb] hits per bucket
+    uint32_t *cur;    // [nb] write cursor per bucket
+    uint32_t *wsum;   // [4] per-wave scan totals
+    uint32_t *off;    // [nb + 1] run starts, then the end
+    uint32_t *tmp;    // [TILE] each packet's hit rule id or ~0u, in tile order
+    uint32_t *ids;    // [hit_reg_words] the tile's ids, bucket by bucket
+};
+
+template <int PPT>
+__device__ __forceinline__ HitLds hit_lds(const CopKParams &p, uint32_t *lds)
+{
+    HitLds h;
+    const uint32_t nb = p.hit_nb;
+    h.cnt = lds + p.lds_hit_off;
+    h.cur = h.cnt + nb;
+    h.wsum = h.cur + nb;
+    h.off = h.wsum + 4;
+    h.tmp = h.cnt + ((3u * nb + 5u + 3u) & ~3u);   // 16-byte aligned
+    h.ids = h.tmp + BLOCK * PPT;
+    return h;
+}
+
+// the tile's FW hits: per-bucket counts (LDS adds; cnt zeroed before the
+// tile) and each packet's rule id parked in LDS, so nothing stays in
+// registers until the sort
+template <int PPT>
+__device__ __forceinline__ void hit_hist(const HitLds &h, const bool (&valid)[PPT], const uint32_t (&flags)[PPT],
+                                         const uint32_t (&fwe)[PPT], int tid, bool one)
+{
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        const bool hit = valid[k] && (flags[k] & COPK_FLAG_FW_HIT);
+        const uint32_t id = fwe[k] & 0x00FFFFFFu;
+        if (hit && !one) atomicAdd(&h.cnt[id >> COPK_HIT_SHIFT], 1u);
+        h.tmp[k * BLOCK + tid] = hit ? id : 0xFFFFFFFFu;
+    }
+}
+
+// After a barrier that follows hit_hist: scan the bucket counts (each run
+// padded to 4 ids), place every hit's rule id in its bucket's run, and write
+// the runs (16-byte stores) and their offsets to the tile's region.
+template <int PPT>
+__device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &h, int tid, int lane, int wave)
+{
+    const uint32_t nb = p.hit_nb;
+    uint32_t total;
+    if (nb == 1) {
+        // one bucket: no sort, the hits in tile order by a block-wide scan
+        // of each lane's hit count (no LDS atomics on one word)
+        uint32_t mine = 0;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) mine += h.tmp[k * BLOCK + tid] != 0xFFFFFFFFu;
+        uint32_t agg;
+        const uint32_t ex = wave_excl_scan(mine, 64, lane, &agg);
+        if (lane == 0) h.wsum[wave] = agg;
+        lds_barrier();
+        uint32_t pos = ex, all = 0;
+        for (int w = 0; w < WAVES; w++) {
+            pos += w < wave ? h.wsum[w] : 0u;
+            all += h.wsum[w];
+        }
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const uint32_t id = h.tmp[k * BLOCK + tid];
+            if (id != 0xFFFFFFFFu) h.ids[pos++] = id;
+        }
+        total = (all + 3u) & ~3u;
+        if ((uint32_t)tid < total - all) h.ids[all + tid] = 0xFFFFFFFFu;
+        if (tid == 0) {
+            h.off[0] = 0;
+            h.off[1] = total;
+        }
+        lds_barrier();
+    } else {
+        const uint32_t c = (uint32_t)tid < nb ? h.cnt[tid] : 0u;
+        const uint32_t v = (c + 3u) & ~3u;
+        uint32_t agg;
+        const uint32_t ex = wave_excl_scan(v, 64, lane, &agg);
+        if (lane == 0) h.wsum[wave] = agg;
+        lds_barrier();
+        uint32_t start = ex;
+        for (int w = 0; w < wave; w++) start += h.wsum[w];
+        if ((uint32_t)tid < nb) {
+            h.off[tid] = start;
+            h.cur[tid] = start;
+            for (uint32_t i = c; i < v; i++) h.ids[start + i] = 0xFFFFFFFFu;
+            if ((uint32_t)tid == nb - 1) h.off[nb] = start + v;
+        }
+        lds_barrier();
+        for (int k = 0; k < PPT; k++) {
+            const uint32_t id = h.tmp[k * BLOCK + tid];
+            if (id != 0xFFFFFFFFu) h.ids[atomicAdd(&h.cur[id >> COPK_HIT_SHIFT], 1u)] = id;
+        }
+        lds_barrier();
+        total = h.off[nb];
+    }
+    uint32_t *reg = p.hit_region + (size_t)blockIdx.x * p.hit_reg_words;
+    for (uint32_t c4 = (uint32_t)tid; c4 < total / 4u; c4 += BLOCK)
+        __builtin_nontemporal_store(*(const u32x4 *)&h.ids[4 * c4], (u32x4 *)&reg[4 * c4]);
+    for (uint32_t q = (uint32_t)tid; q <= nb; q += BLOCK) p.hit_off[(size_t)blockIdx.x * (nb + 1) + q] = h.off[q];
+}
+
 // One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,
 // parse/route, lookups, verdicts, records, ordered compaction and the
 // counter flush. Shared by the one-shot kernel (one tile per workgroup)
@@ -149,7 +253,9 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
     // ---- pass 2 (tbl8 step) and the verdicts ----
     Counts cn;
     pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, cn.total, cn.notv4);
-    rule_hit_atomics<FW, PPT>(o, valid, flags, fwe);
+    const bool bins = EXT && FW != COPK_TBL_OFF && p.hit_region != nullptr;
+    if (bins) hit_hist<PPT>(hit_lds<PPT>(p, lc.s_misc - p.lds_misc_off), valid, flags, fwe, tid, p.hit_nb == 1);
+    else rule_hit_atomics<FW, PPT>(o, valid, flags, fwe);
     if (o.dbg & 8u) {
         uint32_t x = 0;
 #pragma unroll
@@ -179,6 +285,8 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
     uint32_t prx[COPK_MAX_DEMUX_PORTS] = {}, ptx[COPK_MAX_DEMUX_PORTS] = {};
     if (o.port_stats) port_counts<PPT>(o.port_stats, valid, fwd, port, prx, ptx);
     flush_counters(p, o, cn, prx, ptx, lc.s_red, lc.s_ps, tid, lane, wave);
+    // (flush_counters' barrier has landed every hit_hist add)
+    if (bins) hit_sort_out<PPT>(p, hit_lds<PPT>(p, lc.s_misc - p.lds_misc_off), tid, lane, wave);
     STAMP(6);
 }
 

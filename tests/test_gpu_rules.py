@@ -3,7 +3,9 @@ configs[4]: 1M ACL rules + 1M LPM prefixes, 256k batches).
 
 Per packet the pipeline must still be bit-exact (verdict, flags, port,
 route next hop, forward list); the per-rule u64 counters must equal the
-oracle's per-rule hit counts exactly. At 1M rules the oracle runs in its
+oracle's per-rule hit counts exactly, whether they are binned (each tile
+sorts its hits' rule ids by bucket, cop_hit_count adds them up; the
+default) or added by one atomic per hit ($COP_HIT_BINS=0). At 1M rules the oracle runs in its
 rules-only mode (hash probes, no DIR-24-8 image; tests/test_rule_ids.py
 checks that mode against the image mode).
 """
@@ -23,8 +25,10 @@ def fw1k():
     return cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
 
 
+@pytest.mark.parametrize("bins", ["1", "0"], ids=["bins", "atomics"])
 @pytest.mark.parametrize("flags", [0, cg.CFG_FW_FORCE_DIR24], ids=["ivt", "dir24"])
-def test_rule_counters_fw1k(gpu_ctx_factory, flags):
+def test_rule_counters_fw1k(gpu_ctx_factory, flags, bins, monkeypatch):
+    monkeypatch.setenv("COP_HIT_BINS", bins)
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=flags | cg.CFG_RULE_COUNTERS)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
@@ -40,6 +44,33 @@ def test_rule_counters_fw1k(gpu_ctx_factory, flags):
     assert len(got) == o.n_rules
     assert np.array_equal(got, hits), np.nonzero(got != hits)[0][:10]
     assert hits.sum() > 0
+
+
+def test_rule_counters_hot_rule_and_many_buckets(gpu_ctx_factory):
+    """Skewed hits (70 % of the sources inside one rule's prefix) over a
+    100k-rule table (7 buckets of 16384 rule ids), ragged batches: binned
+    counts equal the oracle's."""
+    rules = cg.gen_rules(0x5EED1044, 100000, cg.GEN_FW, 0)
+    t = cg.LpmTable(rules, 100000, 1 << 16, False)
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_RULE_COUNTERS)
+    ctx.set_fw_table(t)
+    o = orc.OracleLpm(100000, 1 << 16, rules_only=True)
+    o.setup(rules["ip"], rules["depth"], rules["next_hop"], stop_at_error=False)
+    n = 3 * 65536 + 4099
+    pk = cg.gen_trace(0x5EED0044, n, rules)
+    hot = rules[rules["depth"] == 24][0]
+    rng = np.random.default_rng(5)
+    sel = rng.random(n) < 0.7
+    src = (int(hot["ip"]) & 0xFFFFFF00) | rng.integers(0, 256, int(sel.sum()))
+    pk.reshape(n, 64)[sel, 26:30] = src.astype(">u4").view(np.uint8).reshape(-1, 4)
+    hits = np.zeros(o.n_rules, np.uint64)
+    ro, fo, _ = orc.process(pk, n, stages=S | F, fw=o, rule_hits=hits)
+    rg, fg, _ = gpu_run(ctx, pk, n, batches=4)
+    assert_parity(rg, fg, ro, fo)
+    got = ctx.rule_counters()
+    assert np.array_equal(got, hits), np.nonzero(got != hits)[0][:10]
+    assert hits.max() > n // 2   # the hot rule
+    assert np.count_nonzero(hits) > 1000
 
 
 def test_rule_counters_accumulate_and_reset(gpu_ctx_factory):

@@ -4,7 +4,8 @@ Tables above 8192 intervals leave LDS for the DIR-24-8 image in HBM (the
 firewall's with rule-id payload, the route stage's with next hops). Records
 must stay bit-identical with thousands of tbl8 groups, a /16 holding 6000
 host routes, /1 prefixes and the two ends of the address space — with the
-default mode selection and with FORCE_DIR24 set explicitly.
+default mode selection, with FORCE_DIR24 set explicitly, and with the
+tbl8 groups in their packed run-block form ($COP_TBL8=packed).
 """
 import numpy as np
 import pytest
@@ -16,7 +17,8 @@ from helpers import assert_parity, gpu_run
 pytestmark = pytest.mark.gpu
 
 S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
-MODES = {"auto": 0, "forced": cg.CFG_FW_FORCE_DIR24 | cg.CFG_LPM_FORCE_DIR24}
+DIR = cg.CFG_FW_FORCE_DIR24 | cg.CFG_LPM_FORCE_DIR24
+MODES = {"auto": (0, "plain"), "forced": (DIR, "plain"), "packed": (DIR, "packed")}
 
 
 def dense_routes():
@@ -37,13 +39,14 @@ def dense_routes():
 
 
 @pytest.mark.parametrize("mode", list(MODES))
-def test_large_fw_and_routes(gpu_ctx_factory, mode):
+def test_large_fw_and_routes(gpu_ctx_factory, mode, monkeypatch):
+    monkeypatch.setenv("COP_TBL8", MODES[mode][1])
     fw_rules = cg.gen_rules(0x5EED1077, 20000, cg.GEN_FW, 0)
     routes = dense_routes()
     fwt = cg.LpmTable(fw_rules, 20000, 1 << 16, False)
     rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
     assert len(fwt.intervals()[0]) > 8192       # leaves LDS
-    ctx = gpu_ctx_factory(stages=S | F | L, flags=MODES[mode] | cg.CFG_RULE_COUNTERS)
+    ctx = gpu_ctx_factory(stages=S | F | L, flags=MODES[mode][0] | cg.CFG_RULE_COUNTERS)
     ctx.set_fw_table(fwt)
     ctx.set_route_lpm(rtt)
     ofw = orc.OracleLpm(20000, 1 << 16)
@@ -74,11 +77,12 @@ def test_large_fw_and_routes(gpu_ctx_factory, mode):
 
 
 @pytest.mark.parametrize("mode", list(MODES))
-def test_large_table_all_addresses_of_a_dense_chunk(gpu_ctx_factory, mode):
+def test_large_table_all_addresses_of_a_dense_chunk(gpu_ctx_factory, mode, monkeypatch):
     """Every address of the dense /16 (65536 lookups) against the oracle."""
+    monkeypatch.setenv("COP_TBL8", MODES[mode][1])
     routes = dense_routes()
     rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
-    ctx = gpu_ctx_factory(stages=S | L, flags=MODES[mode])
+    ctx = gpu_ctx_factory(stages=S | L, flags=MODES[mode][0])
     ctx.set_route_lpm(rtt)
     ort = orc.OracleLpm(1 << 20, 1 << 16)
     ort.setup(routes["ip"], routes["depth"], routes["next_hop"], stop_at_error=False)

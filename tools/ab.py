@@ -5,8 +5,8 @@ bench): every variant is a context created under its own environment
 box-to-box and drift effects cancel, and the median per-launch kernel time
 (HIP events on the launch stream) is reported.
 
-usage: python tools/ab.py [--workload fw1k|fw_lpm|imix] [--rounds 7]
-           [--per-launch 384] [--launches 8] VARIANT...
+usage: python tools/ab.py [--workload fw1k|fw_lpm|imix|fw_lpm_1m] [--rounds 7]
+           [--per-launch 384] [--launches 8] [--rule-counters] VARIANT...
 VARIANT = name[:KEY=VAL[,KEY=VAL...]][/nocompact]
 e.g.  python tools/ab.py base stage0:COP_STAGE_LISTS=0 p8:COP_PPT=8
 """
@@ -35,32 +35,43 @@ def parse_variant(spec):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="fw1k", choices=["fw1k", "fw_lpm", "imix"])
+    ap.add_argument("--workload", default="fw1k", choices=["fw1k", "fw_lpm", "imix", "fw_lpm_1m"])
+    ap.add_argument("--rule-counters", action="store_true", help="per-rule hit counters (COP_CFG_RULE_COUNTERS)")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--per-launch", type=int, default=384)
     ap.add_argument("--launches", type=int, default=8)
     ap.add_argument("variants", nargs="+")
     args = ap.parse_args()
 
-    fw_rules = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
-    routes = cg.gen_rules(0x5EED2004, 100000, cg.GEN_ROUTES, 0) if args.workload != "fw1k" else None
+    big = args.workload == "fw_lpm_1m"   # BASELINE configs[4]: 1M ACL rules + 1M prefixes, 256k batches
+    if big:
+        fw_rules = cg.gen_rules(0x5EED1005, 1000000, cg.GEN_FW, 0)
+        routes = cg.gen_rules(0x5EED2005, 1000000, cg.GEN_ROUTES, 0)
+        fw_tab = cg.LpmTable(fw_rules, 1000000, 1 << 20, False)
+        rt_tab = cg.LpmTable(routes, 1 << 20, 1 << 20, False)
+    else:
+        fw_rules = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
+        routes = cg.gen_rules(0x5EED2004, 100000, cg.GEN_ROUTES, 0) if args.workload != "fw1k" else None
+        fw_tab = cg.LpmTable(fw_rules, 1024, 24, True)
+        rt_tab = cg.LpmTable(routes, 1 << 20, 1 << 16, False) if routes is not None else None
     stages = S | F | (L if routes is not None else 0)
-    B = 65536
+    B = 262144 if big else 65536
+    flags = cg.CFG_RULE_COUNTERS if args.rule_counters else 0
     Lb = args.per_launch
     variants = [parse_variant(v) for v in args.variants]
     ctxs = []
     for name, env, compact in variants:
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        c = cg.Context(stages=stages, max_batch=B, n_streams=1)
+        c = cg.Context(stages=stages, max_batch=B, n_streams=1, flags=flags)
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-        c.set_fw_table(cg.LpmTable(fw_rules, 1024, 24, True))
-        if routes is not None:
-            c.set_route_lpm(cg.LpmTable(routes, 1 << 20, 1 << 16, False))
+        c.set_fw_table(fw_tab)
+        if rt_tab is not None:
+            c.set_route_lpm(rt_tab)
         ctxs.append(c)
     base = ctxs[0]
     if args.workload == "imix":

@@ -49,7 +49,7 @@ def main():
     # their grids; the main launches are the group with the most bytes
     res = {}
     for name in fb_:
-        if "cop_pipeline" not in name:
+        if "cop_pipeline" not in name and "cop_hit_count" not in name:
             continue
         for grid in sorted({g for g, _ in fb_[name]}):
             fv = [v for g, v in fb_[name] if g == grid]
@@ -70,10 +70,15 @@ def main():
         wv = [v for _, v in wb_.get(name, [])] or [0.0]
         pmd[name] = {"dispatches": len(fv), "read_bytes_total": sum(fv) * 1024 * rf,
                      "write_bytes_total": sum(wv) * 1024 * wf}
-    main_k = max(res, key=lambda k: res[k]["total_fetch_kib"])
+    main_k = max((k for k in res if "cop_pipeline" in k), key=lambda k: res[k]["total_fetch_kib"])
     doc = {"kernel": main_k, "hbm_bytes_per_launch": res[main_k]["hbm_bytes_per_launch"],
            "read_bytes_per_launch": res[main_k]["read_bytes"], "write_bytes_per_launch": res[main_k]["write_bytes"],
            "calibration": cal, "kernels": res, "pmd": pmd,
+           # binned per-rule counters: the count kernel after each launch
+           # (the group dispatched as often as the main launches)
+           "hit_count": max(({"kernel": k, **v} for k, v in res.items() if "cop_hit_count" in k),
+                            key=lambda d: (d["dispatches"] == res[main_k]["dispatches"], d["total_fetch_kib"]),
+                            default=None),
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; KiB per dispatch; "
                      "read factor calibrated on tools/membench kA (same access pattern, known bytes)"}
     json.dump(doc, open(out, "w"), indent=1)
