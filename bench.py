@@ -141,8 +141,9 @@ def main():
     ap.add_argument("--streams", type=int, default=1, help="launch lanes (concurrent streams)")
     ap.add_argument("--engine", default="auto", choices=("auto", "pmd", "launch"),
                     help="pmd: the poll-mode kernel serves the batch ring (steps are posted to it); launch: one "
-                         "kernel launch per --per-launch steps; auto: launch when per-rule counters are on (their "
-                         "binned counting runs after each launch), else pmd")
+                         "kernel launch per --per-launch steps; auto: pmd for short runs (< 1024 steps: no "
+                         "per-launch ramp), launch for long runs (large launches stream faster) and whenever "
+                         "per-rule counters are on (their binned counting runs after each launch)")
     ap.add_argument("--pool-mib", type=int, default=0,
                     help="distinct input bytes per GPU (0: max(400 MiB, one launch of batches))")
     ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the value is their median")
@@ -179,7 +180,7 @@ def main():
         fw_tab = cg.LpmTable(fw_rules, W["fw"], 1 << 20, False)
     rc_on = bool(W.get("rule_counters")) and not args.no_rule_counters
     if args.engine == "auto":
-        args.engine = "launch" if rc_on else "pmd"
+        args.engine = "launch" if rc_on or args.steps >= 1024 else "pmd"
     if args.stages:
         W = dict(W, stages=args.stages)
     ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32, n_streams=args.streams,

@@ -141,6 +141,26 @@ def test_edge_versions_and_ports(gpu_ctx_factory):
         assert (v == verdict).sum() > 0, verdict
 
 
+def test_dense_routing_table_lds_fallback(gpu_ctx_factory):
+    """A random routing table with every /8 block non-uniform (256 leaves,
+    128 KiB of LDS) beside the firewall's and a route table's interval
+    images: too much for LDS, so the launch looks the interval tables up in
+    their DIR-24-8 images instead. Results identical."""
+    rules = fw1k()
+    routes = routes100k(n=3000)
+    rng = np.random.default_rng(11)
+    rt = rng.integers(0, 6, 65536).astype(np.uint16)
+    rt[rng.random(65536) < 0.05] = 0xFFFF
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L, routing_table=rt)
+    n = 50000
+    pk = cg.gen_trace(0x5EED0078, n, rules, routes)
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(pk, n, rt=rt, stages=S | F | L, fw=fwo, route=rto)
+    rg, fg, _ = gpu_run(ctx, pk, n)
+    assert_parity(rg, fg, ro, fo)
+    assert (rg["verdict"] == cg.DROP_NO_PORT).sum() > 0 and (rg["verdict"] == cg.DROP_PARSE).sum() > 0
+
+
 @pytest.mark.parametrize("stages", [S, S | F, S | L, F, F | L, S | F | L])
 def test_stage_masks(gpu_ctx_factory, stages):
     rules = fw1k()
