@@ -120,12 +120,15 @@ __device__ __forceinline__ uint32_t eyt_search(const uint32_t *tree, uint32_t le
 }
 
 // Decoupled look-back over one chain of tile granules (tile t at
-// chain[t * stride]): publish this tile's aggregate, read up to 64
-// predecessors per round (lane l reads tile qhi-l), consume the ready prefix
-// up to and including the nearest inclusive prefix, then publish the
-// inclusive value. Granules are {epoch:32, flag:2 (1 aggregate, 2 inclusive),
-// value:30}; a stale epoch counts as not ready. Spins are bounded and report
-// through the host-mapped error word. Whole wave; returns the exclusive prefix.
+// chain[t * stride]): publish this tile's aggregate, read up to 256
+// predecessors per round (four loads per lane: lane l reads tiles qhi-l,
+// qhi-64-l, ...; one round trip resolves a long chain whose tiles have all
+// published), consume the ready prefix up to and including the nearest
+// inclusive prefix, then publish the inclusive value. Granules are
+// {epoch:32, flag:2 (1 aggregate, 2 inclusive), value:30}; a stale epoch
+// counts as not ready. Spins are bounded and report through the host-mapped
+// error word. Whole wave; returns the exclusive prefix.
+constexpr int LB_GROUPS = 4;
 __device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_t stride, uint32_t j, uint32_t agg,
                                               uint32_t epoch, uint32_t *err, int lane)
 {
@@ -139,23 +142,38 @@ __device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_
     int qhi = (int)j - 1;
     uint32_t spins = 0;
     for (;;) {
-        const int idx = qhi - lane;
-        const bool inb = idx >= 0;
-        const unsigned long long v = inb ? lb_load(&chain[(size_t)idx * stride]) : 0ull;
-        const uint32_t flag = (uint32_t)(v >> 30) & 3u;
-        const bool ok = inb && (uint32_t)(v >> 32) == epoch && flag != 0u;
-        const unsigned long long m_incl = __ballot(ok && flag == 2u);
-        const unsigned long long m_bad = __ballot(inb && !ok);
-        const int first_incl = m_incl ? __ffsll((long long)m_incl) - 1 : 64;
-        const int first_bad = m_bad ? __ffsll((long long)m_bad) - 1 : 64;
-        const int upto = min(first_incl + 1, first_bad);
-        uint32_t val = lane < upto ? ((uint32_t)v & 0x3FFFFFFFu) : 0u;
+        unsigned long long v[LB_GROUPS];
 #pragma unroll
-        for (int off = 32; off; off >>= 1) val += __shfl_xor(val, off);
-        excl += val;
-        if (first_incl < first_bad) break;
-        qhi -= upto;
-        if (upto == 0) {
+        for (int r = 0; r < LB_GROUPS; r++) {
+            const int idx = qhi - r * 64 - lane;
+            v[r] = idx >= 0 ? lb_load(&chain[(size_t)idx * stride]) : 0ull;
+        }
+        int consumed = 0;
+        bool done = false;
+#pragma unroll
+        for (int r = 0; r < LB_GROUPS; r++) {
+            const bool inb = qhi - r * 64 - lane >= 0;
+            const uint32_t flag = (uint32_t)(v[r] >> 30) & 3u;
+            const bool ok = inb && (uint32_t)(v[r] >> 32) == epoch && flag != 0u;
+            const unsigned long long m_incl = __ballot(ok && flag == 2u);
+            const unsigned long long m_bad = __ballot(inb && !ok);
+            const int first_incl = m_incl ? __ffsll((long long)m_incl) - 1 : 64;
+            const int first_bad = m_bad ? __ffsll((long long)m_bad) - 1 : 64;
+            const int upto = min(first_incl + 1, first_bad);
+            uint32_t val = lane < upto ? ((uint32_t)v[r] & 0x3FFFFFFFu) : 0u;
+#pragma unroll
+            for (int off = 32; off; off >>= 1) val += __shfl_xor(val, off);
+            excl += val;
+            consumed += upto;
+            if (first_incl < first_bad) {
+                done = true;
+                break;
+            }
+            if (upto < 64) break;   // a predecessor not ready yet: re-read from it
+        }
+        if (done) break;
+        qhi -= consumed;
+        if (consumed == 0) {
             if (++spins > (1u << 22)) {       // bounded: never hang the GPU
                 if (lane == 0) *err = 1u;
                 break;

@@ -78,6 +78,7 @@ struct CopKParams {
     uint32_t stages;
     uint32_t n_ports;
     uint32_t compact;
+    uint32_t static_order;    // tile j of a batch = its blockIdx order (small launches: no ticket atomics)
     uint32_t epoch;
     uint32_t dbg;             // timing-only ablations ($COP_DBG), 0 in production
     // vport routing table (two-level image)

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(BLOCK, EXT ? 4 : COPK_WAVES_PER_EU) void cop_pipeli
 
     // ---- tile index inside the batch: this batch's ticket counter (or the
     // static order when no look-back runs: p.compact == 0) ----
-    const bool dyn = p.compact != 0 && !(o.dbg & 2u);
+    const bool dyn = p.compact != 0 && !(o.dbg & 2u) && !p.static_order;
     unsigned long long tk = 0;
     if (dyn && tid == 0) tk = atomicAdd(&p.tickets[b * 16], 1ull);
 

@@ -174,6 +174,7 @@ struct cop_ctx {
     bool coalesced = true;     // one-shot kernel: coalesced header loads where eligible ($COP_LOADS=strided: off)
     bool stage_lists = true;   // one-shot kernel: forward lists staged in LDS ($COP_STAGE_LISTS=0: off)
     bool hit_bins = true;      // per-rule hit counters by binning ($COP_HIT_BINS=0: one atomic per hit)
+    bool static_small = true;  // small launches in blockIdx tile order ($COP_STATIC_ORDER=0: tickets)
     uint32_t dbg = 0;          // $COP_DBG: timing-only kernel ablations
     uint32_t lds_pad = 0;      // $COP_LDS_PAD: extra LDS bytes per workgroup (occupancy experiments)
     unsigned long long *stamps = nullptr;   // dbg bit 8: per-workgroup phase stamps
@@ -476,6 +477,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_LOADS")) c->coalesced = strcmp(e, "strided") != 0;
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
     if (const char *e = getenv("COP_HIT_BINS")) c->hit_bins = atoi(e) != 0;
+    if (const char *e = getenv("COP_STATIC_ORDER")) c->static_small = atoi(e) != 0;
     if (const char *e = getenv("COP_STREAMS")) {
         int v = atoi(e);
         if (v >= 1 && v <= MAX_LANES) cfg.n_streams = (uint32_t)v;
@@ -883,6 +885,12 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     p.err = c->d_err + 4 * (&L - c->lane);
     if ((c->dbg & 8u) && p.ntiles > COPK_STAMP_WG) p.dbg &= ~8u;
     const uint32_t grid = p.ntiles;   // one tile per workgroup
+    // Small launches (at most 4 workgroups per CU) take tile j of a batch in
+    // blockIdx order: a look-back then waits only on workgroups dispatched
+    // before it, as with tickets, without the ticket atomics that one batch's
+    // workgroups would all issue on one counter (~3 us for 256 of them).
+    // Large launches keep tickets. ($COP_STATIC_ORDER=0: always tickets)
+    p.static_order = (grid <= 4u * (uint32_t)c->ncu && c->static_small) ? 1u : 0u;
     // per-rule hit counters by binning: each tile sorts its hits' rule ids by
     // bucket into its region, cop_hit_count adds them up after the launch
     p.hit_region = nullptr;
@@ -930,7 +938,7 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     if (p.hit_region && (e = copk_hit_count(&p, grid, COPK_BLOCK * (uint32_t)ppt, L.s)) != hipSuccess)
         return set_err(c, -EIO, "hit count launch: %s", hipGetErrorString(e));
     L.dirty[q ^ 1] = 0;
-    L.dirty[q] = (p.compact && !(c->dbg & 2u)) ? nb_used : 0;
+    L.dirty[q] = (p.compact && !(c->dbg & 2u) && !p.static_order) ? nb_used : 0;
     L.parity = q ^ 1;
     if (c->timing) {
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][1], L.s));
