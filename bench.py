@@ -150,6 +150,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-rule-counters", action="store_true", help="ablation: config 5 without per-rule counters")
+    ap.add_argument("--no-rccl-check", action="store_true",
+                    help="skip the untimed RCCL all-reduce of the ranks' counters at the end")
     ap.add_argument("--stages", type=int, default=0, help="ablation: override the workload's stage mask")
     ap.add_argument("--no-compact", action="store_true", help="ablation: no ordered forward lists")
     args = ap.parse_args()
@@ -364,6 +366,26 @@ def main():
     ctx.launch_timing(False)
     single_batch = {"batch": B, "launches": n_lat, "kernel_us_mean": round(lat_ms * 1e3, 2),
                     "host_submit_to_sync_us_median": round(float(np.median(host_us)), 2)}
+
+    # ---- the ranks' counters summed by RCCL over xGMI (print_stats' totals of
+    # every coprocessor, switch.c:33-90), checked against the packets each rank
+    # ran since the reset above; untimed, and a failure is reported, not fatal
+    allreduce_check = None
+    if not rc_on and not args.no_rccl_check:
+        try:
+            ctx.sync()
+            uid = group.broadcast_bytes(cg.coll_unique_id() if rank == 0 else None)
+            ctx.coll_init(uid, rank, world)
+            group.barrier()
+            r0 = time.perf_counter()
+            tot, _ = ctx.coll_reduce_counters(reset=False, with_rules=False)
+            r_ms = (time.perf_counter() - r0) * 1e3
+            want = world * (nl * Lb + n_lat) * B
+            allreduce_check = {"ranks": world, "u64_words": SHARD_AND_PORT_WORDS, "ms": round(group.max(r_ms), 3),
+                               "rx_sum": int(tot["rx"]), "rx_expected": want, "ok": int(tot["rx"]) == want}
+        except Exception as e:   # noqa: BLE001 (reported in the line)
+            allreduce_check = {"ranks": world, "error": str(e)[:200]}
+        log(f"[rank {rank}] rccl counter check: {allreduce_check}")
     fwd_frac = cnt["forward"] / max(1, cnt["rx"])
     # algorithmic bytes per packet: the 64 B header line (+4 B offset for
     # IMIX), the 8 B result record, and 4 B per forwarded packet for the
@@ -456,6 +478,8 @@ def main():
         out["pmd"] = pmd_info
     if reduce_info:
         out["counter_reduce"] = reduce_info
+    if allreduce_check:
+        out["counter_allreduce_check"] = allreduce_check
 
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
