@@ -318,13 +318,27 @@ def main():
             t0 = time.perf_counter()
             pmd.run(1)
             lat.append((time.perf_counter() - t0) * 1e6)
+        # a producer that posts one batch per call and keeps up to `depth`
+        # in flight (waits only for the oldest): the rate a deployment handing
+        # over single 64k batches gets
+        depth = min(16, P)
+        n_one = min(P * 2, 512)
+        t0 = time.perf_counter()
+        for _ in range(n_one):
+            if pmd.posted >= depth:
+                pmd.wait(pmd.posted - depth + 1)
+            pmd.post(1)
+        pmd.wait()
+        t_one = time.perf_counter() - t0
         info = pmd.info()
         t_long = float(np.median(longs))
         pmd_info = {"workers": info["workers"], "workers_per_cu": info["workers_per_cu"],
                     "packets_per_tile": info["packets_per_tile"], "launches": info["launches"],
                     "steady_batches": n_long, "steady_mpkt_s": round(n_long * B / t_long / 1e6, 3),
                     "steady_ms": round(t_long * 1e3, 4),
-                    "single_batch_post_to_done_us_median": round(float(np.median(lat)), 2)}
+                    "single_batch_post_to_done_us_median": round(float(np.median(lat)), 2),
+                    "one_batch_posts": {"batches": n_one, "in_flight": depth,
+                                        "mpkt_s": round(n_one * B / t_one / 1e6, 3)}}
         pmd_off()
 
     reduce_info = None
