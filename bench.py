@@ -154,6 +154,9 @@ def main():
                     help="skip the untimed RCCL all-reduce of the ranks' counters at the end")
     ap.add_argument("--stages", type=int, default=0, help="ablation: override the workload's stage mask")
     ap.add_argument("--no-compact", action="store_true", help="ablation: no ordered forward lists")
+    ap.add_argument("--route-form", default="dir", choices=("dir", "trie"),
+                    help="route tables too large for LDS: DIR-24-8 image (HBM / Infinity Cache) or the multibit "
+                         "trie (12-bit LDS top level + L2-resident 6-bit nodes)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -186,7 +189,8 @@ def main():
     if args.stages:
         W = dict(W, stages=args.stages)
     ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32, n_streams=args.streams,
-                     flags=(cg.CFG_RULE_COUNTERS if rc_on else 0) | (cg.CFG_NO_COMPACT if args.no_compact else 0))
+                     flags=(cg.CFG_RULE_COUNTERS if rc_on else 0) | (cg.CFG_NO_COMPACT if args.no_compact else 0)
+                     | (cg.CFG_LPM_TRIE if args.route_form == "trie" else 0))
     ctx.set_fw_table(fw_tab)
     if rc_on:
         # RCCL communicator over the GPUs of the job (xGMI); id from rank 0 over gloo
@@ -448,6 +452,7 @@ def main():
             "streams": args.streams,
             "fw_rules": W["fw"],
             "route_prefixes": W["routes"],
+            "route_form": args.route_form if W["routes"] else None,
             "pkt_layout": "imix slab + u32 offsets" if W["imix"] else "64B slots",
             "stages": W["stages"],
             "parallelism": f"independent per-GPU contexts x{world} (no data-path collective)",

@@ -24,7 +24,7 @@ FLAG_ROUTE_HIT, FLAG_FW_HIT = 0x1, 0x2
 COUNTER_SHARDS = 256   # COP_COUNTER_SHARDS
 LPM_STOP_AT_FIRST_ERROR = 0x1
 CFG_FW_FORCE_DIR24, CFG_LPM_FORCE_DIR24, CFG_NO_COMPACT, CFG_RULE_COUNTERS = 0x1, 0x2, 0x4, 0x8
-CFG_DEMUX_PORTS, CFG_PORT_STATS = 0x10, 0x20
+CFG_DEMUX_PORTS, CFG_PORT_STATS, CFG_LPM_TRIE = 0x10, 0x20, 0x40
 MAX_DEMUX_PORTS = 8
 GEN_FW, GEN_ROUTES = 0, 1
 UNKNOWN_PORT = 0xFFFF
@@ -356,6 +356,21 @@ class LpmTable:
         v = np.zeros(m, dtype=np.uint32)
         _check(lib().cop_lpm_export_intervals(self.handle, _ptr(s), _ptr(v), m))
         return s, v
+
+    def trie_probe(self, ips: np.ndarray, form: int = 0):
+        """The multibit-trie form (lpm_trie.c) of this table's device image
+        (form 0: next hop, 1: rule id), walked on the host: (trie values,
+        interval-search values, nodes, leaves) for each address."""
+        ips = np.ascontiguousarray(ips, dtype=np.uint32)
+        out = np.zeros(len(ips), dtype=np.uint32)
+        ref = np.zeros(len(ips), dtype=np.uint32)
+        nn, nl = ctypes.c_uint32(), ctypes.c_uint32()
+        f = lib().cop_lpm_trie_probe
+        f.restype = c_int
+        f.argtypes = [c_void_p, c_int, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]
+        _check(f(self.handle, form, _ptr(ips), len(ips), _ptr(out), _ptr(ref), byref(nn), byref(nl)),
+               what="cop_lpm_trie_probe")
+        return out, ref, nn.value, nl.value
 
     def dir24(self):
         t24 = np.zeros(1 << 24, dtype=np.uint32)

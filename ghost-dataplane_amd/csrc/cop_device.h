@@ -419,7 +419,64 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
         if (FW == COPK_TBL_DIR) fwe[k] = reach ? p.fw_tbl24[src[k] >> 8] : 0u;
         if (LPM == COPK_TBL_IVT) lpe[k] = t.lp_v[eyt_search(t.lp_s, lp_lv, dst[k])];
         if (LPM == COPK_TBL_DIR) lpe[k] = reach ? p.lpm_tbl24[dst[k] >> 8] : 0u;
+        if (LPM == COPK_TBL_TRIE) lpe[k] = t.lp_s[dst[k] >> 20];
     }
+}
+
+// The trie form's walk below its LDS top level (lpm_trie.c): e = the level-0
+// entry, a node (bit 31) or already the value. Per level every live lane's
+// PPT node loads (24 bytes: a dwordx4 and a dwordx2) are issued before any
+// is used; a lane leaves at its first leaf child, whose value is loaded in
+// one last round. Nodes and leaves are small enough to stay in the XCD's L2.
+template <int PPT>
+__device__ __forceinline__ void trie_walk(const uint32_t *nodes, const uint32_t *leaves, const uint32_t (&ip)[PPT],
+                                          uint32_t (&e)[PPT], const bool (&live)[PPT])
+{
+    bool in[PPT], lf[PPT];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        in[k] = live[k] && (e[k] & 0x80000000u);
+        lf[k] = false;
+        any |= in[k];
+    }
+#pragma unroll
+    for (int l = 0; l < 4; l++) {
+        if (!__ballot(any)) break;
+        const uint32_t sh = l == 0 ? 14u : l == 1 ? 8u : l == 2 ? 2u : 0u;
+        const uint32_t msk = l == 3 ? 3u : 63u;
+        u32x4a a[PPT];
+        u32x2a b[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            if (in[k]) {
+                const uint32_t *nd = nodes + (size_t)(e[k] & 0x7FFFFFFFu) * 6u;
+                a[k] = *(const u32x4a *)nd;
+                b[k] = *(const u32x2a *)(nd + 4);
+            }
+        }
+        any = false;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            if (in[k]) {
+                const uint32_t c = (ip[k] >> sh) & msk;
+                const unsigned long long vec = a[k].x | ((unsigned long long)a[k].y << 32);
+                const unsigned long long lv = a[k].z | ((unsigned long long)a[k].w << 32);
+                const unsigned long long upto = (2ull << c) - 1ull;   // c == 63: all ones
+                if ((vec >> c) & 1ull) {
+                    e[k] = 0x80000000u | (b[k].x + (uint32_t)__popcll(vec & upto) - 1u);
+                    any = true;
+                } else {
+                    e[k] = b[k].y + (uint32_t)__popcll(lv & upto) - 1u;
+                    in[k] = false;
+                    lf[k] = true;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PPT; k++)
+        if (lf[k]) e[k] = leaves[e[k]];
 }
 
 // rte_lpm_lookup's tbl8 step for valid+extended tbl24 entries e[k]: a
@@ -473,6 +530,7 @@ __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[
     }
     if (FW == COPK_TBL_DIR) tbl8_step<PPT>(p.fw_tbl8, p.fw_tbl8_packed, src, fwe);
     if (LPM == COPK_TBL_DIR) tbl8_step<PPT>(p.lpm_tbl8, p.lpm_tbl8_packed, dst, lpe);
+    if (LPM == COPK_TBL_TRIE) trie_walk<PPT>(p.lpm_tnodes, p.lpm_tleaves, dst, lpe, reached);
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         if (!reached[k]) continue;
@@ -541,6 +599,53 @@ __device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base,
             c.noport += verdict[k] == COPK_DROP_NO_PORT;
             c.rhit += flags[k] & COPK_FLAG_ROUTE_HIT;
         }
+    }
+}
+
+// The poll-mode kernel's records without an LDS stage: each wave writes its
+// own packets' records as 16-byte write-through stores straight from
+// registers. The records of (step k, wave) are 64 consecutive 8-byte slots;
+// for two steps at a time, lane i < 32 gathers records 2i and 2i+1 of step k
+// and lane 32 + i those of step k+1 (four ds_bpermute per step), so one
+// store instruction writes 1 KiB contiguous per step pair. No barrier: waves
+// 1..3 store while wave 0 looks back. An odd last record takes an 8-byte
+// store. Counts as store_records.
+template <int PPT>
+__device__ __forceinline__ void store_records_paired(const CopKBatch &B, uint32_t base, int tid, int lane, int wave,
+                                                     const bool (&valid)[PPT], const uint32_t (&verdict)[PPT],
+                                                     const uint32_t (&flags)[PPT], const uint32_t (&port)[PPT],
+                                                     const uint32_t (&rnh)[PPT], bool (&fwd)[PPT], Counts &c)
+{
+    uint32_t rx[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        fwd[k] = valid[k] && verdict[k] == COPK_FORWARD;
+        rx[k] = verdict[k] | (flags[k] << 8) | (port[k] << 16);
+        if (valid[k]) {
+            c.rx++;
+            c.fwd += verdict[k] == COPK_FORWARD;
+            c.dropfw += verdict[k] == COPK_DROP_FW;
+            c.parse += verdict[k] == COPK_DROP_PARSE;
+            c.noport += verdict[k] == COPK_DROP_NO_PORT;
+            c.rhit += flags[k] & COPK_FLAG_ROUTE_HIT;
+        }
+    }
+    (void)tid;
+    uint32_t *r = (uint32_t *)B.results;
+    const int i = lane & 31;
+    const bool hi = lane >= 32;
+#pragma unroll
+    for (int k = 0; k < PPT; k += 2) {
+        const int k1 = k + 1 < PPT ? k + 1 : k;
+        const uint32_t a0 = (uint32_t)__shfl((int)rx[k], 2 * i), a1 = (uint32_t)__shfl((int)rnh[k], 2 * i);
+        const uint32_t a2 = (uint32_t)__shfl((int)rx[k], 2 * i + 1), a3 = (uint32_t)__shfl((int)rnh[k], 2 * i + 1);
+        const uint32_t b0 = (uint32_t)__shfl((int)rx[k1], 2 * i), b1 = (uint32_t)__shfl((int)rnh[k1], 2 * i);
+        const uint32_t b2 = (uint32_t)__shfl((int)rx[k1], 2 * i + 1), b3 = (uint32_t)__shfl((int)rnh[k1], 2 * i + 1);
+        if (hi && k1 == k) continue;   // PPT 1: one step, lanes 0..31 store it
+        const uint32_t idx = base + (uint32_t)(hi ? k1 : k) * BLOCK + (uint32_t)wave * 64u + 2u * (uint32_t)i;
+        const u32x4 v = hi ? u32x4{b0, b1, b2, b3} : u32x4{a0, a1, a2, a3};
+        if (idx + 1 < B.n) st_u32x4<true>(v, r, 2 * (long)idx);
+        else if (idx < B.n) st_u32x2<true>(u32x2{v.x, v.y}, (u32x2 *)&r[2 * (size_t)idx]);
     }
 }
 
@@ -739,10 +844,14 @@ __device__ __forceinline__ void port_counts(uint32_t K, const bool (&valid)[PPT]
 // workgroup, into one of COPK_COUNTER_SHARDS shards (a 128-byte line each)
 // so no single word serialises thousands of atomics; then the per-port
 // counters the same way. s_red: WAVES*8 words, s_ps: WAVES*16 words.
-__device__ __forceinline__ void flush_counters(const CopKParams &p, const Opt &o, const Counts &cn,
-                                               const uint32_t (&prx)[COPK_MAX_DEMUX_PORTS],
-                                               const uint32_t (&ptx)[COPK_MAX_DEMUX_PORTS], uint32_t *s_red,
-                                               uint32_t *s_ps, int tid, int lane, int wave)
+// Split in two: flush_counters_lds (wave reduce into LDS) and, after a
+// workgroup barrier, flush_counters_add (the sums and the atomics). The
+// poll-mode kernel runs the second half after it has signalled the tile, so
+// the tile's store drain never waits behind counter atomics.
+__device__ __forceinline__ void flush_counters_lds(const Opt &o, const Counts &cn,
+                                                   const uint32_t (&prx)[COPK_MAX_DEMUX_PORTS],
+                                                   const uint32_t (&ptx)[COPK_MAX_DEMUX_PORTS], uint32_t *s_red,
+                                                   uint32_t *s_ps, int lane, int wave)
 {
     uint32_t c[8] = {cn.total, cn.notv4, cn.fwd, cn.dropfw, cn.parse, cn.noport, cn.rhit, cn.rx};
 #pragma unroll
@@ -765,7 +874,12 @@ __device__ __forceinline__ void flush_counters(const CopKParams &p, const Opt &o
             s_ps[wave * 16 + 2 * q + 1] = ptx[q];
         }
     }
-    lds_barrier();
+}
+
+__device__ __forceinline__ void flush_counters_add(const CopKParams &p, const Opt &o, const uint32_t *s_red,
+                                                   const uint32_t *s_ps, int tid)
+{
+    const uint32_t K = o.port_stats;
     if (tid < 9) {
         uint32_t r[8];
 #pragma unroll
@@ -798,6 +912,16 @@ __device__ __forceinline__ void flush_counters(const CopKParams &p, const Opt &o
         if (v)
             atomicAdd(&p.port_ctr[(blockIdx.x % COPK_COUNTER_SHARDS) * COPK_PORT_WORDS + tid], (unsigned long long)v);
     }
+}
+
+__device__ __forceinline__ void flush_counters(const CopKParams &p, const Opt &o, const Counts &cn,
+                                               const uint32_t (&prx)[COPK_MAX_DEMUX_PORTS],
+                                               const uint32_t (&ptx)[COPK_MAX_DEMUX_PORTS], uint32_t *s_red,
+                                               uint32_t *s_ps, int tid, int lane, int wave)
+{
+    flush_counters_lds(o, cn, prx, ptx, s_red, s_ps, lane, wave);
+    lds_barrier();
+    flush_counters_add(p, o, s_red, s_ps, tid);
 }
 
 }  // namespace copd

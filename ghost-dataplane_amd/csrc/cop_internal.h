@@ -67,6 +67,26 @@ uint32_t cop_lpm_merged_intervals(const cop_lpm_table *t, uint32_t **starts, uin
  * tbl8: t->n_ext * 256 entries). */
 void cop_lpm_fill_dir24(const cop_lpm_table *t, uint32_t *tbl24, uint32_t *tbl8);
 
+/* Multibit-trie device form (lpm_trie.c): a 12-bit top level (LDS), then
+ * popcount-compressed 6-bit nodes of COP_TRIE_NODE_WORDS u32 and a leaf
+ * array (L2-resident). Level-0 entries with COP_TRIE_NODE set are nodes. */
+#define COP_TRIE_L0 4096u
+#define COP_TRIE_NODE 0x80000000u
+#define COP_TRIE_NODE_WORDS 6u
+typedef struct {
+    uint32_t l0[COP_TRIE_L0];
+    uint32_t n_nodes, n_leaves;
+    uint32_t *nodes;    /* n_nodes * COP_TRIE_NODE_WORDS */
+    uint32_t *leaves;
+} cop_lpm_trie;
+int cop_lpm_trie_build(const uint32_t *starts, const uint32_t *vals, uint32_t m, cop_lpm_trie *out);
+void cop_lpm_trie_free(cop_lpm_trie *t);
+uint32_t cop_lpm_trie_lookup(const cop_lpm_trie *t, uint32_t ip);
+/* tests: the trie of a table's form; per ip the trie walk (out) and the
+ * interval search (ref); node and leaf counts */
+int cop_lpm_trie_probe(const cop_lpm_table *tab, int form, const uint32_t *ips, uint32_t n, uint32_t *out,
+                       uint32_t *ref, uint32_t *n_nodes, uint32_t *n_leaves);
+
 /* Host paths with an explicit stage mask instead of the context's: the
  * drop-in coprocessor API (dropin.c) runs the coprocessor thread's NF chain,
  * COP_DROPIN_STAGES (process_packet, coprocessor.c:50-65). */

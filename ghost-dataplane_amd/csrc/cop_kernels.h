@@ -21,6 +21,8 @@ static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_TBL_OFF 0
 #define COPK_TBL_IVT 1  /* flattened intervals, binary search in LDS */
 #define COPK_TBL_DIR 2  /* DIR-24-8 image in HBM */
+#define COPK_TBL_TRIE 3 /* multibit trie: 12-bit top level in LDS, 6-bit popcount nodes in L2 (route stage) */
+#define COPK_TRIE_L0 4096u
 /* Packed tbl8 form of a DIR-24-8 image: an extended tbl24 entry's payload is
  * the offset (in 64-byte units) of its /24's run block instead of a group
  * index. A block describes the group's 256 entries as runs of equal
@@ -95,10 +97,14 @@ struct CopKParams {
     const uint32_t *lpm_starts, *lpm_vals;
     const uint32_t *lpm_tbl24, *lpm_tbl8;
     uint32_t lpm_tbl8_packed;
+    const uint32_t *lpm_tl0;     // trie form (lpm_trie.c): 4096 top entries (staged in LDS)
+    const uint32_t *lpm_tnodes;  // 6 u32 per node: vec, leafvec (u64 each), child_base, leaf_base
+    const uint32_t *lpm_tleaves;
     // LDS carve (u32 words)
     uint32_t lds_fw_off, lds_lpm_off, lds_misc_off;
     uint32_t lds_stage_off;   // one-shot kernel: the tile's forward list staged in LDS (0: none)
     uint32_t lds_rec_off;     // poll-mode kernel: the tile's records staged in LDS (0: none)
+    uint32_t rec_paired;      // poll-mode kernel: records as 16-byte stores from lane pairs, no LDS stage
     // ordering / accounting state
     unsigned long long *tickets;   // one counter per batch, one 128-byte line each (zero at launch)
     unsigned long long *zero_tickets;  // the lane's other ticket buffer: zeroed by this launch
@@ -142,6 +148,7 @@ struct CopKPmd {
     uint32_t n_work;                     // worker workgroups
     uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
     uint32_t idle_ticks;                 // s_memrealtime ticks (100 MHz) without a post before leaving
+    uint32_t defer_ctr;                  // add a tile's counters after signalling it (0: before, $COP_PMD_DEFER_CTR=0)
 };
 #define COPK_PMD_RELAYS 8
 #define COPK_PMD_RUNNING 0u

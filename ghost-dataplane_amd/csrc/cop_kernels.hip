@@ -134,17 +134,36 @@ hipError_t launch_lpm(const CopKParams &p, int lpm, int imix, int ppt, uint32_t 
 {
     if (lpm == COPK_TBL_IVT) return launch_imix<FW, COPK_TBL_IVT>(p, imix, ppt, grid, lds, s);
     if (lpm == COPK_TBL_DIR) return launch_imix<FW, COPK_TBL_DIR>(p, imix, ppt, grid, lds, s);
+    if (lpm == COPK_TBL_TRIE) return launch_imix<FW, COPK_TBL_TRIE>(p, imix, ppt, grid, lds, s);
     return launch_imix<FW, COPK_TBL_OFF>(p, imix, ppt, grid, lds, s);
 }
 
 } // namespace
 
+// The kernel's instantiations are compiled in three parts, one per firewall
+// table mode (COPK_FW_PART = 0, 1, 2: this file built three more times), so
+// the build runs in parallel; the part-less build holds the dispatcher and
+// the small kernels.
+#define COPK_LAUNCH_ARGS const CopKParams *p, int lpm_mode, int imix, int ppt, uint32_t grid, uint32_t lds_bytes, \
+                         hipStream_t stream
+extern "C" hipError_t copk_launch_fw0(COPK_LAUNCH_ARGS);
+extern "C" hipError_t copk_launch_fw1(COPK_LAUNCH_ARGS);
+extern "C" hipError_t copk_launch_fw2(COPK_LAUNCH_ARGS);
+#if defined(COPK_FW_PART)
+#define COPK_CAT2(a, b) a##b
+#define COPK_CAT(a, b) COPK_CAT2(a, b)
+extern "C" hipError_t COPK_CAT(copk_launch_fw, COPK_FW_PART)(COPK_LAUNCH_ARGS)
+{
+    return launch_lpm<COPK_FW_PART>(*p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
+}
+#else
+static_assert(COPK_TBL_OFF == 0 && COPK_TBL_IVT == 1 && COPK_TBL_DIR == 2, "part numbering");
 extern "C" hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int imix, int ppt,
                                   uint32_t grid, uint32_t lds_bytes, hipStream_t stream)
 {
-    if (fw_mode == COPK_TBL_IVT) return launch_lpm<COPK_TBL_IVT>(*p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
-    if (fw_mode == COPK_TBL_DIR) return launch_lpm<COPK_TBL_DIR>(*p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
-    return launch_lpm<COPK_TBL_OFF>(*p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
+    if (fw_mode == COPK_TBL_IVT) return copk_launch_fw1(p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
+    if (fw_mode == COPK_TBL_DIR) return copk_launch_fw2(p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
+    return copk_launch_fw0(p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
 }
 
 namespace {
@@ -235,3 +254,4 @@ extern "C" hipError_t copk_snapshot(unsigned long long *src, uint32_t n_words, u
     hipLaunchKernelGGL(cop_snapshot, dim3((n_words + 255) / 256), dim3(256), 0, stream, src, n_words, dst, reset);
     return hipGetLastError();
 }
+#endif  // COPK_FW_PART

@@ -60,7 +60,7 @@ __device__ __forceinline__ void pmd_leave(const CopKPmd &P, uint32_t why)
 // not one per worker, and no workgroup slot spent on a doorbell. Leaders
 // also turn the host's stop flag, a look-back timeout or an idle spell
 // (no new post for idle_ticks) into the exit word.
-__device__ unsigned long long wait_posted(const CopKPmd &P, unsigned long long b, bool leader)
+__device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd &P, unsigned long long b, bool leader)
 {
     // this worker's copy of the relay (one 128-byte line per XCD-sized
     // group of workers): a thousand pollers on one line would hammer one
@@ -181,9 +181,12 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
         uint32_t look_off;
         const CopKBatch B = batch_desc(p, slot, &look_off);
+        // counters are added after the tile is signalled (defer_ctr), unless
+        // the tile bins rule hits (their sort needs the counters' barrier)
+        const bool defer = P.defer_ctr && !(EXT && p.hit_region);
         tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(p, o, lc, B, look_off, j,
                                                 LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2]}, tid_i, lane_i,
-                                                wave_i, false);
+                                                wave_i, false, defer);
         // completion: every wave's stores (write-through) have landed, then
         // one lane counts the tile; the slot's last tile signals the host
         if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done
@@ -198,6 +201,9 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                 st_stamp(&stamp[5], (old + 1) % tpb == 0 ? 1ull : 0ull);
             }
         }
+        // the tile's counters (reduced into LDS by tile_body, ordered by the
+        // barrier above); the next tile rewrites that LDS only after barriers
+        if (defer) flush_counters_add(p, o, lc.s_red, lc.s_ps, tid);
         // next tile: T += G
         j += rb;
         uint32_t db = qb;
@@ -246,18 +252,32 @@ hipError_t pmd_lpm(const CopKPmd *p, int lpm, int lay, int ppt, int ext, uint32_
 {
     if (lpm == COPK_TBL_IVT) return pmd_lay<FW, COPK_TBL_IVT>(p, lay, ppt, ext, lds, s, occ);
     if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);
+    if (lpm == COPK_TBL_TRIE) return pmd_lay<FW, COPK_TBL_TRIE>(p, lay, ppt, ext, lds, s, occ);
     return pmd_lay<FW, COPK_TBL_OFF>(p, lay, ppt, ext, lds, s, occ);
 }
 
-hipError_t pmd_dispatch(const CopKPmd *p, int fw, int lpm, int lay, int ppt, int ext, uint32_t lds, hipStream_t s,
-                        int *occ)
-{
-    if (fw == COPK_TBL_IVT) return pmd_lpm<COPK_TBL_IVT>(p, lpm, lay, ppt, ext, lds, s, occ);
-    if (fw == COPK_TBL_DIR) return pmd_lpm<COPK_TBL_DIR>(p, lpm, lay, ppt, ext, lds, s, occ);
-    return pmd_lpm<COPK_TBL_OFF>(p, lpm, lay, ppt, ext, lds, s, occ);
-}
-
 }  // namespace
+
+// compiled in three parts, one per firewall table mode (as cop_kernels.hip)
+#define COPK_PMD_ARGS const CopKPmd *p, int lpm, int lay, int ppt, int ext, uint32_t lds, hipStream_t s, int *occ
+extern "C" hipError_t copk_pmd_fw0(COPK_PMD_ARGS);
+extern "C" hipError_t copk_pmd_fw1(COPK_PMD_ARGS);
+extern "C" hipError_t copk_pmd_fw2(COPK_PMD_ARGS);
+#if defined(COPK_FW_PART)
+#define COPK_CAT2(a, b) a##b
+#define COPK_CAT(a, b) COPK_CAT2(a, b)
+extern "C" hipError_t COPK_CAT(copk_pmd_fw, COPK_FW_PART)(COPK_PMD_ARGS)
+{
+    return pmd_lpm<COPK_FW_PART>(p, lpm, lay, ppt, ext, lds, s, occ);
+}
+#else
+static hipError_t pmd_dispatch(const CopKPmd *p, int fw, int lpm, int lay, int ppt, int ext, uint32_t lds,
+                               hipStream_t s, int *occ)
+{
+    if (fw == COPK_TBL_IVT) return copk_pmd_fw1(p, lpm, lay, ppt, ext, lds, s, occ);
+    if (fw == COPK_TBL_DIR) return copk_pmd_fw2(p, lpm, lay, ppt, ext, lds, s, occ);
+    return copk_pmd_fw0(p, lpm, lay, ppt, ext, lds, s, occ);
+}
 
 extern "C" hipError_t copk_pmd_launch(const CopKPmd *p, int fw_mode, int lpm_mode, int layout, int ppt, int ext,
                                       uint32_t lds_bytes, hipStream_t stream)
@@ -271,3 +291,4 @@ extern "C" hipError_t copk_pmd_occupancy(int fw_mode, int lpm_mode, int layout, 
     *per_cu = 0;
     return pmd_dispatch(nullptr, fw_mode, lpm_mode, layout, ppt, ext, lds_bytes, nullptr, per_cu);
 }
+#endif  // COPK_FW_PART

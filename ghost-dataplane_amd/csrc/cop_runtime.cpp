@@ -48,6 +48,9 @@ struct DevLpm {
     uint32_t n_ext = 0;
     bool tbl8_packed = false;       // tbl8 as packed run blocks (COPK_TBL_DIR form note)
     size_t tbl8_bytes = 0;
+    // multibit-trie form (lpm_trie.c): top level, nodes, leaves; null if not built
+    uint32_t *tl0 = nullptr, *tnodes = nullptr, *tleaves = nullptr;
+    uint32_t t_nodes = 0, t_leaves = 0;
 };
 
 struct Lane {
@@ -299,6 +302,9 @@ static void free_lpm(DevLpm &t)
     if (t.vals) (void)hipFree(t.vals);
     if (t.tbl24) (void)hipFree(t.tbl24);
     if (t.tbl8) (void)hipFree(t.tbl8);
+    if (t.tl0) (void)hipFree(t.tl0);
+    if (t.tnodes) (void)hipFree(t.tnodes);
+    if (t.tleaves) (void)hipFree(t.tleaves);
     t = DevLpm();
 }
 
@@ -478,6 +484,11 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
     if (const char *e = getenv("COP_HIT_BINS")) c->hit_bins = atoi(e) != 0;
     if (const char *e = getenv("COP_STATIC_ORDER")) c->static_small = atoi(e) != 0;
+    // route-table form for tables too large for LDS (A/B runs): trie | dir
+    if (const char *e = getenv("COP_LPM_FORM")) {
+        if (!strcmp(e, "trie")) c->cfg.flags |= COP_CFG_LPM_TRIE;
+        else if (!strcmp(e, "dir")) c->cfg.flags &= ~COP_CFG_LPM_TRIE;
+    }
     if (const char *e = getenv("COP_STREAMS")) {
         int v = atoi(e);
         if (v >= 1 && v <= MAX_LANES) cfg.n_streams = (uint32_t)v;
@@ -597,7 +608,27 @@ static void pack_tbl8(std::vector<uint32_t> &h24, std::vector<uint32_t> &h8)
     h8.swap(blk);
 }
 
-static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt, int form)
+// the multibit-trie form of intervals (s, v, m) into t (COP_CFG_LPM_TRIE)
+static int upload_trie(cop_ctx *c, DevLpm &t, const uint32_t *s, const uint32_t *v, uint32_t m)
+{
+    cop_lpm_trie tr;
+    int rc = cop_lpm_trie_build(s, v, m, &tr);
+    if (rc) return set_err(c, rc, "trie build failed: %d", rc);
+    const size_t nb = (size_t)std::max(tr.n_nodes, 1u) * COP_TRIE_NODE_WORDS * 4, lb = (size_t)std::max(tr.n_leaves, 1u) * 4;
+    hipError_t e = hipMalloc(&t.tl0, COP_TRIE_L0 * 4);
+    if (e == hipSuccess) e = hipMalloc(&t.tnodes, nb);
+    if (e == hipSuccess) e = hipMalloc(&t.tleaves, lb);
+    if (e == hipSuccess) e = hipMemcpy(t.tl0, tr.l0, COP_TRIE_L0 * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(t.tnodes, tr.nodes, nb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(t.tleaves, tr.leaves, lb, hipMemcpyHostToDevice);
+    t.t_nodes = tr.n_nodes;
+    t.t_leaves = tr.n_leaves;
+    cop_lpm_trie_free(&tr);
+    if (e != hipSuccess) return set_err(c, -ENOMEM, "trie upload: %s", hipGetErrorString(e));
+    return 0;
+}
+
+static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt, int form, bool want_trie = false)
 {
     if (int rc = sync_lanes(c)) return rc;
     free_lpm(t);
@@ -636,8 +667,11 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
         HIPCHK(c, hipMemcpy(t.vals, hv.data(), M * 4, hipMemcpyHostToDevice));
         t.m = M;
     }
+    int trc = 0;
+    if (want_trie && !t.m) trc = upload_trie(c, t, s, v, m);   // too large for the LDS interval form
     free(s);
     free(v);
+    if (trc) return trc;
     // DIR-24-8 image (always: FORCE_DIR24 and the large-table path)
     const uint32_t n_ext = cop_lpm_form_n_ext(tab, form);
     std::vector<uint32_t> h24((size_t)1 << 24);
@@ -690,7 +724,8 @@ int cop_set_route_lpm(cop_ctx *c, const cop_lpm_table *t)
 {
     if (!c || !t) return -EINVAL;
     if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel is serving this context (cop_pmd_stop first)");
-    return upload_lpm(c, c->lpm, t, !(c->cfg.flags & COP_CFG_LPM_FORCE_DIR24), COP_FORM_NH);
+    return upload_lpm(c, c->lpm, t, !(c->cfg.flags & COP_CFG_LPM_FORCE_DIR24), COP_FORM_NH,
+                      (c->cfg.flags & COP_CFG_LPM_TRIE) != 0);
 }
 
 int cop_load_fw_rules_file(cop_ctx *c, const char *path, const cop_lpm_config *cfg,
@@ -713,6 +748,7 @@ static int pick_mode(const cop_ctx *c, const DevLpm &t, bool enabled, bool force
 {
     if (!enabled) return COPK_TBL_OFF;
     if (!force_dir && t.m) return COPK_TBL_IVT;
+    if (!force_dir && t.tl0) return COPK_TBL_TRIE;
     if (t.tbl24) return COPK_TBL_DIR;
     return COPK_TBL_IVT;  // empty table (m = 4)
 }
@@ -794,7 +830,8 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     const bool stage_list = p.compact && !p.demux && c->stage_lists;
     auto lds_need = [&](int fwm, int lpmm) {
         return (256u + c->rt_nleaf * 128u + (fwm == COPK_TBL_IVT ? 2u * c->fw.m : 0u) +
-                (lpmm == COPK_TBL_IVT ? 2u * c->lpm.m : 0u) + misc_words + (stage_list ? COPK_BLOCK * ppt : 0u) +
+                (lpmm == COPK_TBL_IVT ? 2u * c->lpm.m : lpmm == COPK_TBL_TRIE ? COPK_TRIE_L0 : 0u) + misc_words +
+                (stage_list ? COPK_BLOCK * ppt : 0u) +
                 (stage_records ? 2u * COPK_BLOCK * ppt : 0u)) *
                    4u +
                c->lds_pad;
@@ -803,7 +840,7 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     // tables): look the interval tables up in their DIR-24-8 images in HBM
     // instead, the route stage's first. Results are identical.
     while (lds_need(fw_mode, lpm_mode) > 160u * 1024u) {
-        if (lpm_mode == COPK_TBL_IVT && c->lpm.tbl24) lpm_mode = COPK_TBL_DIR;
+        if ((lpm_mode == COPK_TBL_IVT || lpm_mode == COPK_TBL_TRIE) && c->lpm.tbl24) lpm_mode = COPK_TBL_DIR;
         else if (fw_mode == COPK_TBL_IVT && c->fw.tbl24) fw_mode = COPK_TBL_DIR;
         else return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_need(fw_mode, lpm_mode));
     }
@@ -819,11 +856,14 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     p.lpm_tbl24 = c->lpm.tbl24;
     p.lpm_tbl8 = c->lpm.tbl8;
     p.lpm_tbl8_packed = c->lpm.tbl8_packed ? 1u : 0u;
+    p.lpm_tl0 = c->lpm.tl0;
+    p.lpm_tnodes = c->lpm.tnodes;
+    p.lpm_tleaves = c->lpm.tleaves;
     uint32_t off = 256 + c->rt_nleaf * 128;
     p.lds_fw_off = off;
     off += 2 * p.fw_m;
     p.lds_lpm_off = off;
-    off += 2 * p.lpm_m;
+    off += lpm_mode == COPK_TBL_TRIE ? COPK_TRIE_L0 : 2 * p.lpm_m;
     p.lds_misc_off = off;
     off += misc_words;
     p.lds_stage_off = 0;
@@ -1804,9 +1844,14 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
     {
         // records as 16-byte write-through stores from LDS: every slot's
         // records 16-byte aligned
-        const bool stage_rec = !getenv("COP_PMD_NO_REC_STAGE") && ((uintptr_t)r->results & 15) == 0 &&
-                               (r->results_slot & 1) == 0;
+        // ($COP_PMD_REC: paired = from lane pairs in registers, the default;
+        // stage = through an LDS stage after the compaction; 8 = 8-byte stores)
+        const char *rec_env = getenv("COP_PMD_REC");
+        const bool wide = ((uintptr_t)r->results & 15) == 0 && (r->results_slot & 1) == 0 &&
+                          !(rec_env && !strcmp(rec_env, "8"));
+        const bool stage_rec = wide && rec_env && !strcmp(rec_env, "stage");
         if ((rc = fill_launch(c, p, ppt, &m->fw_mode, &m->lpm_mode, &m->lds_bytes, stage_rec))) goto fail;
+        p.rec_paired = wide && !stage_rec ? 1u : 0u;
         p.dbg = 0;   // no ablations in the persistent kernel
         p.stamps = nullptr;
         const char *stamps_env = getenv("COP_PMD_STAMPS");
@@ -1829,6 +1874,7 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         m->per_cu = (uint32_t)occ;
         pmd_size(m);
         m->P.idle_ticks = 100000000u;   // 1 s at 100 MHz
+        m->P.defer_ctr = getenv("COP_PMD_DEFER_CTR") && !atoi(getenv("COP_PMD_DEFER_CTR")) ? 0u : 1u;
         if (const char *env = getenv("COP_PMD_IDLE_MS")) m->P.idle_ticks = (uint32_t)strtoul(env, nullptr, 0) * 100000u;
         // control block in mapped host memory
         const size_t ctl_bytes = 64 + (size_t)m->n_slots * 8;

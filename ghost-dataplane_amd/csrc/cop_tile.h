@@ -70,6 +70,7 @@ __device__ __forceinline__ void stage_tables(const CopKParams &p, const Tables &
         lds_stage(tb.lp_s, p.lpm_starts, p.lpm_m >> 2, lane, wave);
         lds_stage(tb.lp_v, p.lpm_vals, p.lpm_m >> 2, lane, wave);
     }
+    if (LPM == COPK_TBL_TRIE) lds_stage(tb.lp_s, p.lpm_tl0, COPK_TRIE_L0 / 4u, lane, wave);
 }
 
 // Per-rule hit binning (CopKParams::hit_region): the LDS of the tile's sort
@@ -185,7 +186,7 @@ __device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &
 template <int FW, int LPM, int LAY, int PPT, bool EXT, bool WT>
 __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, const LdsCarve &lc, const CopKBatch &B,
                                           uint32_t look_off, uint32_t j, const LookCtx &lk, int tid, int lane, int wave,
-                                          bool sync_tables)
+                                          bool sync_tables, bool defer_ctr = false)
 {
     constexpr bool IMIX = LAY == COPK_LAY_IMIX;
     const Tables &tb = lc.tb;
@@ -269,8 +270,10 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
 #pragma unroll
     for (int k = 0; k < PPT; k++) fwd[k] = valid[k] && verdict[k] == COPK_FORWARD;
     uint32_t *rec_stage = (WT && p.lds_rec_off) ? lc.s_misc - p.lds_misc_off + p.lds_rec_off : nullptr;
+    const bool paired = WT && p.rec_paired;
     auto records = [&] {
-        store_records<PPT, WT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn, rec_stage);
+        if (paired) store_records_paired<PPT>(B, base, tid, lane, wave, valid, verdict, flags, port, rnh, fwd, cn);
+        else store_records<PPT, WT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn, rec_stage);
     };
     if (p.compact) compact_tile<PPT, WT>(lk, o, B, look_off, j, base, fwd, port, lc.cl, tid, lane, wave, records);
     else records();
@@ -284,9 +287,14 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
     // ---- counters (one flush per workgroup) ----
     uint32_t prx[COPK_MAX_DEMUX_PORTS] = {}, ptx[COPK_MAX_DEMUX_PORTS] = {};
     if (o.port_stats) port_counts<PPT>(o.port_stats, valid, fwd, port, prx, ptx);
-    flush_counters(p, o, cn, prx, ptx, lc.s_red, lc.s_ps, tid, lane, wave);
-    // (flush_counters' barrier has landed every hit_hist add)
-    if (bins) hit_sort_out<PPT>(p, hit_lds<PPT>(p, lc.s_misc - p.lds_misc_off), tid, lane, wave);
+    if (defer_ctr && !bins) {
+        // the caller adds them (flush_counters_add) after a barrier of its own
+        flush_counters_lds(o, cn, prx, ptx, lc.s_red, lc.s_ps, lane, wave);
+    } else {
+        flush_counters(p, o, cn, prx, ptx, lc.s_red, lc.s_ps, tid, lane, wave);
+        // (flush_counters' barrier has landed every hit_hist add)
+        if (bins) hit_sort_out<PPT>(p, hit_lds<PPT>(p, lc.s_misc - p.lds_misc_off), tid, lane, wave);
+    }
     STAMP(6);
 }
 

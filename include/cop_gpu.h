@@ -205,6 +205,10 @@ typedef struct cop_ctx cop_ctx;
 #define COP_CFG_DEMUX_PORTS     0x10u
 /* Per-port coprocessor_stats (switch.h:33-38) kept on the device. */
 #define COP_CFG_PORT_STATS      0x20u
+/* Route tables too large for LDS: look them up in the multibit-trie form
+ * (12-bit top level in LDS, popcount-compressed 6-bit nodes, a few MiB that
+ * stay in L2) instead of the 64 MiB DIR-24-8 image. Results are identical. */
+#define COP_CFG_LPM_TRIE        0x40u
 #define COP_MAX_DEMUX_PORTS     8
 
 typedef struct cop_config {

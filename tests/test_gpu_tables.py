@@ -4,8 +4,9 @@ Tables above 8192 intervals leave LDS for the DIR-24-8 image in HBM (the
 firewall's with rule-id payload, the route stage's with next hops). Records
 must stay bit-identical with thousands of tbl8 groups, a /16 holding 6000
 host routes, /1 prefixes and the two ends of the address space — with the
-default mode selection, with FORCE_DIR24 set explicitly, and with the
-tbl8 groups in their packed run-block form ($COP_TBL8=packed).
+default mode selection, with FORCE_DIR24 set explicitly, with the
+tbl8 groups in their packed run-block form ($COP_TBL8=packed), and with the
+route stage in its multibit-trie form (CFG_LPM_TRIE).
 """
 import numpy as np
 import pytest
@@ -18,7 +19,9 @@ pytestmark = pytest.mark.gpu
 
 S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
 DIR = cg.CFG_FW_FORCE_DIR24 | cg.CFG_LPM_FORCE_DIR24
-MODES = {"auto": (0, "plain"), "forced": (DIR, "plain"), "packed": (DIR, "packed")}
+# trie: the route stage in its multibit-trie form (LDS top level + L2 nodes)
+MODES = {"auto": (0, "plain"), "forced": (DIR, "plain"), "packed": (DIR, "packed"),
+         "trie": (cg.CFG_LPM_TRIE, "plain")}
 
 
 def dense_routes():

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Short-run (20-step) experiments: bench variants and the poll-mode probe.
+# usage: tools/exp_short.sh <outdir-name> [variant...]   variants: base nocompact cu4 probe probe2
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+out=$R/gpurun_out/${1:-exp_short}; shift
+mkdir -p "$out"
+step() { "$R/tools/gpu_step.sh" "$@" || exit 99; }
+for v in "$@"; do
+  case $v in
+    base) step 200 "$out/bench20_base.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 ;;
+    nocompact) step 200 "$out/bench20_nocompact.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 --no-compact ;;
+    cu4) COP_PMD_PER_CU=4 step 200 "$out/bench20_cu4.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 ;;
+    probe) COP_PMD_STAMPS=1 step 200 "$out/probe.log" python3 -u "$R/tools/pmd_probe.py" --posts 1,20 ;;
+    probe2) COP_PMD_STAMPS=2 step 200 "$out/probe2.log" python3 -u "$R/tools/pmd_probe.py" --posts 1,20 ;;
+    recstage) COP_PMD_REC=stage step 200 "$out/bench20_recstage.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 ;;
+    pmdtests) step 300 "$out/pytest_pmd.log" python3 -u -m pytest "$R/tests/test_gpu_pmd.py" -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    gputests) step 600 "$out/pytest_gpu.log" python3 -u -m pytest "$R/tests" -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    nodefer) COP_PMD_DEFER_CTR=0 step 200 "$out/bench20_nodefer.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 ;;
+    tabletests) step 300 "$out/pytest_tables.log" python3 -u -m pytest "$R/tests/test_gpu_tables.py" -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    abtrie) step 300 "$out/ab_trie_fw_lpm_L1024.log" python3 -u "$R/tools/ab.py" --workload fw_lpm --per-launch 1024 --rounds 5 --launches 4 dir trie:COP_LPM_FORM=trie ;;
+    abtrie_imix) step 300 "$out/ab_trie_imix_L384.log" python3 -u "$R/tools/ab.py" --workload imix --per-launch 384 --rounds 5 --launches 4 dir trie:COP_LPM_FORM=trie ;;
+    abtrie_1m) step 300 "$out/ab_trie_fw_lpm_1m_L25.log" python3 -u "$R/tools/ab.py" --workload fw_lpm_1m --per-launch 25 --rounds 5 --launches 8 dir trie:COP_LPM_FORM=trie ;;
+    launch) step 200 "$out/bench20_launch.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 --engine launch ;;
+  esac
+done
