@@ -86,9 +86,14 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
                 seen = h;
                 t_seen = now;
             }
-            if (ld_agent(&P.d_ctl[2])) pmd_leave(P, COPK_PMD_ABORT);   // a look-back timed out
-            else if (__hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) pmd_leave(P, COPK_PMD_STOPPED);
-            else if (now - t_seen > P.idle_ticks) pmd_leave(P, COPK_PMD_IDLE);
+            // the exit checks every 16th poll: the stop flag is a second
+            // PCIe read, and the doorbell is polled once per round trip
+            if ((spins & 15u) == 15u) {
+                if (ld_agent(&P.d_ctl[2])) pmd_leave(P, COPK_PMD_ABORT);   // a look-back timed out
+                else if (__hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+                    pmd_leave(P, COPK_PMD_STOPPED);
+                else if (now - t_seen > P.idle_ticks) pmd_leave(P, COPK_PMD_IDLE);
+            }
         } else {
             // back off to ~0.5 us between polls while nothing comes
             for (uint32_t k = spins < 16 ? 0u : 3u; k; k--) __builtin_amdgcn_s_sleep(4);

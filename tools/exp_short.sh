@@ -21,6 +21,12 @@ for v in "$@"; do
     abtrie) step 300 "$out/ab_trie_fw_lpm_L1024.log" python3 -u "$R/tools/ab.py" --workload fw_lpm --per-launch 1024 --rounds 5 --launches 4 dir trie:COP_LPM_FORM=trie ;;
     abtrie_imix) step 300 "$out/ab_trie_imix_L384.log" python3 -u "$R/tools/ab.py" --workload imix --per-launch 384 --rounds 5 --launches 4 dir trie:COP_LPM_FORM=trie ;;
     abtrie_1m) step 300 "$out/ab_trie_fw_lpm_1m_L25.log" python3 -u "$R/tools/ab.py" --workload fw_lpm_1m --per-launch 25 --rounds 5 --launches 8 dir trie:COP_LPM_FORM=trie ;;
+    ppt1) COP_PPT=1 step 200 "$out/bench20_ppt1.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 5 ;;
+
+    ppt4) COP_PPT=4 step 200 "$out/bench20_ppt4.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 5 ;;
+    ppt8) COP_PPT=8 step 200 "$out/bench20_ppt8.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 5 ;;
+    relay16) COP_PMD_RELAY_STRIDE=16 step 200 "$out/bench20_relay16.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 ;;
+    relay256) COP_PMD_RELAY_STRIDE=256 step 200 "$out/bench20_relay256.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 ;;
     launch) step 200 "$out/bench20_launch.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 --engine launch ;;
   esac
 done
