@@ -64,10 +64,14 @@ def test_fw_dir24_forced(gpu_ctx_factory):
     assert_parity(rg, fg, ro, fo)
 
 
-def test_fw_lpm_100k(gpu_ctx_factory):
+FORMS = {"dir": 0, "trie": cg.CFG_LPM_TRIE}   # the 100k route table: DIR-24-8 or the multibit trie
+
+
+@pytest.mark.parametrize("form", list(FORMS))
+def test_fw_lpm_100k(gpu_ctx_factory, form):
     rules = fw1k()
     routes = routes100k()
-    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L)
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L, flags=FORMS[form])
     n = 65536
     pk = cg.gen_trace(0x5EED0003, n, rules, routes)
     fwo, rto = oracle_tables(rules, routes)
@@ -77,10 +81,11 @@ def test_fw_lpm_100k(gpu_ctx_factory):
     assert (rg["flags"] & cg.FLAG_ROUTE_HIT).sum() > n // 10   # the route stage really hits
 
 
-def test_imix_fw_lpm(gpu_ctx_factory):
+@pytest.mark.parametrize("form", list(FORMS))
+def test_imix_fw_lpm(gpu_ctx_factory, form):
     rules = fw1k()
     routes = routes100k()
-    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L)
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L, flags=FORMS[form])
     n = 65536
     slab, offs = cg.gen_imix(0x5EED0003, n, rules, routes)
     fwo, rto = oracle_tables(rules, routes)

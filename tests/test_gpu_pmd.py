@@ -160,11 +160,13 @@ def test_pmd_layouts(gpu_ctx_factory, layout):
     check(*rg.read(), ro, fos, B, P)
 
 
-def test_pmd_imix(gpu_ctx_factory):
-    """IMIX slab + u32 offsets per slot."""
+@pytest.mark.parametrize("form", ["dir", "trie"])
+def test_pmd_imix(gpu_ctx_factory, form):
+    """IMIX slab + u32 offsets per slot; the 20k-route table (beyond LDS) as
+    DIR-24-8 or in the multibit-trie form."""
     rules = fw1k()
     rts = routes(20000)
-    ctx = gpu_ctx_factory(stages=S | F | L)
+    ctx = gpu_ctx_factory(stages=S | F | L, flags=cg.CFG_LPM_TRIE if form == "trie" else 0)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     ctx.set_route_lpm(cg.LpmTable(rts, 1 << 20, 1 << 16, False))
     B, P = 20000, 3
@@ -192,12 +194,15 @@ def test_pmd_imix(gpu_ctx_factory):
         assert int(cnt[s]) == len(f1) and np.array_equal(fwd[s * B:s * B + len(f1)], f1)
 
 
-def test_pmd_dir24_rule_counters(gpu_ctx_factory):
-    """FW and route stage both DIR-24-8 in HBM, per-rule hit counters (the
-    EXT kernel): counters equal the oracle's hits over every posted batch."""
+@pytest.mark.parametrize("form", ["dir", "trie"])
+def test_pmd_dir24_rule_counters(gpu_ctx_factory, form):
+    """FW stage DIR-24-8 in HBM, the route stage DIR-24-8 or trie, per-rule
+    hit counters (the EXT kernel): counters equal the oracle's hits over
+    every posted batch."""
     rules = fw1k()
     rts = routes()
-    ctx = gpu_ctx_factory(stages=S | F | L, flags=cg.CFG_FW_FORCE_DIR24 | cg.CFG_RULE_COUNTERS)
+    ctx = gpu_ctx_factory(stages=S | F | L, flags=cg.CFG_FW_FORCE_DIR24 | cg.CFG_RULE_COUNTERS
+                          | (cg.CFG_LPM_TRIE if form == "trie" else 0))
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     ctx.set_route_lpm(cg.LpmTable(rts, 1 << 20, 1 << 16, False))
     B, P = 65536, 6
