@@ -92,6 +92,43 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Several LDS-DMA copies in ONE loop over their 1 KiB pieces (piece q of
+// the concatenation: its segment picked by scalar compares). The compiler
+// puts an s_waitcnt vmcnt(0) in front of every separate LDS-DMA loop (the
+// DMA writes LDS that an earlier one may have written), which serialised
+// the table staging into one memory round trip per table: 2-3 us at the
+// start of every workgroup. One loop has one wait, before any load.
+struct StageSeg {
+    const void *g;      // global source (16-byte aligned)
+    uint32_t *dst;      // LDS destination
+    uint32_t n16;       // 16-byte chunks (0: unused)
+};
+
+// up to six segments, passed by value and selected by compares (an indexed
+// array of them would live in scratch memory, whose loads also wait on vmcnt)
+__device__ __forceinline__ void lds_stage_all(StageSeg s0, StageSeg s1, StageSeg s2, StageSeg s3, StageSeg s4,
+                                              StageSeg s5, int lane, int wave)
+{
+    const uint32_t f1 = (s0.n16 + 63u) >> 6;
+    const uint32_t f2 = f1 + ((s1.n16 + 63u) >> 6);
+    const uint32_t f3 = f2 + ((s2.n16 + 63u) >> 6);
+    const uint32_t f4 = f3 + ((s3.n16 + 63u) >> 6);
+    const uint32_t f5 = f4 + ((s4.n16 + 63u) >> 6);
+    const uint32_t total = f5 + ((s5.n16 + 63u) >> 6);
+    for (uint32_t q = (uint32_t)wave; q < total; q += WAVES) {
+        // field by field (selecting whole structs by reference puts them in scratch)
+        const bool b1 = q >= f1, b2 = q >= f2, b3 = q >= f3, b4 = q >= f4, b5 = q >= f5;
+        const void *g = b5 ? s5.g : b4 ? s4.g : b3 ? s3.g : b2 ? s2.g : b1 ? s1.g : s0.g;
+        uint32_t *dst = b5 ? s5.dst : b4 ? s4.dst : b3 ? s3.dst : b2 ? s2.dst : b1 ? s1.dst : s0.dst;
+        const uint32_t n16 = b5 ? s5.n16 : b4 ? s4.n16 : b3 ? s3.n16 : b2 ? s2.n16 : b1 ? s1.n16 : s0.n16;
+        const uint32_t c = q - (b5 ? f5 : b4 ? f4 : b3 ? f3 : b2 ? f2 : b1 ? f1 : 0u);
+        const uint32_t i = c * 64u + (uint32_t)lane;
+        if (i < n16)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)((const uint4 *)g + i),
+                                             (__attribute__((address_space(3))) void *)(dst + c * 256u), 16, 0, 0);
+    }
+}
+
 __device__ __forceinline__ void lds_stage(uint32_t *lds_dst, const void *gsrc, uint32_t n16, int lane, int wave)
 {
     // one 1 KiB piece per wave-instruction: LDS destination = base + lane*16
@@ -610,7 +647,7 @@ __device__ __forceinline__ void store_records(const CopKBatch &B, uint32_t base,
 // store instruction writes 1 KiB contiguous per step pair. No barrier: waves
 // 1..3 store while wave 0 looks back. An odd last record takes an 8-byte
 // store. Counts as store_records.
-template <int PPT>
+template <int PPT, bool WT>
 __device__ __forceinline__ void store_records_paired(const CopKBatch &B, uint32_t base, int tid, int lane, int wave,
                                                      const bool (&valid)[PPT], const uint32_t (&verdict)[PPT],
                                                      const uint32_t (&flags)[PPT], const uint32_t (&port)[PPT],
@@ -644,8 +681,8 @@ __device__ __forceinline__ void store_records_paired(const CopKBatch &B, uint32_
         if (hi && k1 == k) continue;   // PPT 1: one step, lanes 0..31 store it
         const uint32_t idx = base + (uint32_t)(hi ? k1 : k) * BLOCK + (uint32_t)wave * 64u + 2u * (uint32_t)i;
         const u32x4 v = hi ? u32x4{b0, b1, b2, b3} : u32x4{a0, a1, a2, a3};
-        if (idx + 1 < B.n) st_u32x4<true>(v, r, 2 * (long)idx);
-        else if (idx < B.n) st_u32x2<true>(u32x2{v.x, v.y}, (u32x2 *)&r[2 * (size_t)idx]);
+        if (idx + 1 < B.n) st_u32x4<WT>(v, r, 2 * (long)idx);
+        else if (idx < B.n) st_u32x2<WT>(u32x2{v.x, v.y}, (u32x2 *)&r[2 * (size_t)idx]);
     }
 }
 

@@ -48,6 +48,22 @@ using namespace copd;
 // header records, one 16-byte load per packet: the end-to-end host path)
 // EXT: the launch uses an optional feature (demux, port stats, per-rule
 // counters, $COP_DBG ablations); without, their code is compiled out.
+// The batch's ticket: a returning device-scope add, waited for inside the
+// same asm block. As a plain atomicAdd its pending result register made the
+// compiler put an s_waitcnt vmcnt(0) in front of the header loads on the
+// ticket-free path too (one merged wait state for both paths), so every
+// small launch's workgroups waited for their LDS-DMA table staging before
+// loading a packet.
+__device__ __forceinline__ __attribute__((unused)) unsigned long long ticket_take(unsigned long long *p)
+{
+    unsigned long long old;
+    asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)"
+                 : "=v"(old)
+                 : "v"(p), "v"(1ull)
+                 : "memory");
+    return old;
+}
+
 template <int FW, int LPM, int LAY, int PPT, bool EXT>
 __global__ __launch_bounds__(BLOCK, EXT ? 4 : COPK_WAVES_PER_EU) void cop_pipeline(const CopKParams p)
 {
@@ -65,6 +81,10 @@ __global__ __launch_bounds__(BLOCK, EXT ? 4 : COPK_WAVES_PER_EU) void cop_pipeli
     // tile's predecessors have normally published their counts by the time
     // its look-back reads them. Unequal batches: blockIdx ranges.
     const uint32_t g = blockIdx.x;
+    // ---- stage tables into LDS by LDS-DMA first: the loads go out before
+    // anything else is in flight (no wait in front of them), and land while
+    // the ticket and the header loads are in flight ----
+    if (!(o.dbg & 4u)) stage_tables<FW, LPM>(p, lc.tb, lane, wave);
     const bool ilv = p.uniform_ntiles != 0 && !(o.dbg & 256u);
     const uint32_t b = ilv ? __builtin_amdgcn_readfirstlane(g % p.nb) : batch_of_tile(p, g);
     uint32_t look_off;
@@ -84,10 +104,8 @@ __global__ __launch_bounds__(BLOCK, EXT ? 4 : COPK_WAVES_PER_EU) void cop_pipeli
     // static order when no look-back runs: p.compact == 0) ----
     const bool dyn = p.compact != 0 && !(o.dbg & 2u) && !p.static_order;
     unsigned long long tk = 0;
-    if (dyn && tid == 0) tk = atomicAdd(&p.tickets[b * 16], 1ull);
+    if (dyn && tid == 0) tk = ticket_take(&p.tickets[b * 16]);
 
-    // ---- stage tables into LDS by LDS-DMA while the ticket is in flight ----
-    if (!(o.dbg & 4u)) stage_tables<FW, LPM>(p, lc.tb, lane, wave);
     uint32_t j;
     if (dyn) {
         if (tid == 0) *lc.s_tile = (uint32_t)tk;

@@ -178,6 +178,7 @@ struct cop_ctx {
     bool stage_lists = true;   // one-shot kernel: forward lists staged in LDS ($COP_STAGE_LISTS=0: off)
     bool hit_bins = true;      // per-rule hit counters by binning ($COP_HIT_BINS=0: one atomic per hit)
     bool static_small = true;  // small launches in blockIdx tile order ($COP_STATIC_ORDER=0: tickets)
+    bool rec_paired = false;   // one-shot kernel: records as 16-byte stores from lane pairs ($COP_REC_PAIRED=1)
     uint32_t dbg = 0;          // $COP_DBG: timing-only kernel ablations
     uint32_t lds_pad = 0;      // $COP_LDS_PAD: extra LDS bytes per workgroup (occupancy experiments)
     unsigned long long *stamps = nullptr;   // dbg bit 8: per-workgroup phase stamps
@@ -484,6 +485,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
     if (const char *e = getenv("COP_HIT_BINS")) c->hit_bins = atoi(e) != 0;
     if (const char *e = getenv("COP_STATIC_ORDER")) c->static_small = atoi(e) != 0;
+    if (const char *e = getenv("COP_REC_PAIRED")) c->rec_paired = atoi(e) != 0;
     // route-table form for tables too large for LDS (A/B runs): trie | dir
     if (const char *e = getenv("COP_LPM_FORM")) {
         if (!strcmp(e, "trie")) c->cfg.flags |= COP_CFG_LPM_TRIE;
@@ -911,6 +913,16 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     int fw_mode = 0, lpm_mode = 0;
     uint32_t lds_bytes = 0;
     if (int rc = fill_launch(c, p, ppt, &fw_mode, &lpm_mode, &lds_bytes)) return rc;
+    // records as 16-byte stores from lane pairs ($COP_REC_PAIRED=1): every
+    // batch's records must start 16-byte aligned
+    p.rec_paired = 0;
+    if (c->rec_paired) {
+        bool al = true;
+        if (p.ring) al = ((uintptr_t)p.rg.results & 15) == 0 && (p.rg.results_slot & 1) == 0;
+        else
+            for (uint32_t i = 0; i < p.nb; i++) al = al && ((uintptr_t)p.b[i].results & 15) == 0;
+        p.rec_paired = al ? 1u : 0u;
+    }
     if (++L.epoch == 0) {
         HIPCHK(c, hipMemsetAsync(L.look, 0, (size_t)L.look_cap * 8, L.s));
         L.epoch = 1;

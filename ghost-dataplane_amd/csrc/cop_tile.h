@@ -57,20 +57,18 @@ __device__ __forceinline__ LdsCarve lds_carve(const CopKParams &p, uint32_t *lds
 
 // Stage the vport route image and the interval tables into LDS by LDS-DMA
 // (completion: the caller's __syncthreads()).
+// (one LDS-DMA loop for all of them: lds_stage_all)
 template <int FW, int LPM>
 __device__ __forceinline__ void stage_tables(const CopKParams &p, const Tables &tb, int lane, int wave)
 {
-    lds_stage(tb.rt_top, p.rt_top, 64, lane, wave);
-    lds_stage((uint32_t *)tb.rt_leaf, p.rt_leaf, p.rt_nleaf * 32u, lane, wave);
-    if (FW == COPK_TBL_IVT) {
-        lds_stage(tb.fw_s, p.fw_starts, p.fw_m >> 2, lane, wave);
-        lds_stage(tb.fw_v, p.fw_vals, p.fw_m >> 2, lane, wave);
-    }
-    if (LPM == COPK_TBL_IVT) {
-        lds_stage(tb.lp_s, p.lpm_starts, p.lpm_m >> 2, lane, wave);
-        lds_stage(tb.lp_v, p.lpm_vals, p.lpm_m >> 2, lane, wave);
-    }
-    if (LPM == COPK_TBL_TRIE) lds_stage(tb.lp_s, p.lpm_tl0, COPK_TRIE_L0 / 4u, lane, wave);
+    constexpr bool fw = FW == COPK_TBL_IVT, lpm = LPM == COPK_TBL_IVT, trie = LPM == COPK_TBL_TRIE;
+    const StageSeg none{nullptr, nullptr, 0u};
+    lds_stage_all(StageSeg{p.rt_top, tb.rt_top, 64u}, StageSeg{p.rt_leaf, (uint32_t *)tb.rt_leaf, p.rt_nleaf * 32u},
+                  fw ? StageSeg{p.fw_starts, tb.fw_s, p.fw_m >> 2} : none,
+                  fw ? StageSeg{p.fw_vals, tb.fw_v, p.fw_m >> 2} : none,
+                  lpm ? StageSeg{p.lpm_starts, tb.lp_s, p.lpm_m >> 2}
+                      : trie ? StageSeg{p.lpm_tl0, tb.lp_s, COPK_TRIE_L0 / 4u} : none,
+                  lpm ? StageSeg{p.lpm_vals, tb.lp_v, p.lpm_m >> 2} : none, lane, wave);
 }
 
 // Per-rule hit binning (CopKParams::hit_region): the LDS of the tile's sort
@@ -270,9 +268,9 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
 #pragma unroll
     for (int k = 0; k < PPT; k++) fwd[k] = valid[k] && verdict[k] == COPK_FORWARD;
     uint32_t *rec_stage = (WT && p.lds_rec_off) ? lc.s_misc - p.lds_misc_off + p.lds_rec_off : nullptr;
-    const bool paired = WT && p.rec_paired;
+    const bool paired = p.rec_paired != 0;
     auto records = [&] {
-        if (paired) store_records_paired<PPT>(B, base, tid, lane, wave, valid, verdict, flags, port, rnh, fwd, cn);
+        if (paired) store_records_paired<PPT, WT>(B, base, tid, lane, wave, valid, verdict, flags, port, rnh, fwd, cn);
         else store_records<PPT, WT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn, rec_stage);
     };
     if (p.compact) compact_tile<PPT, WT>(lk, o, B, look_off, j, base, fwd, port, lc.cl, tid, lane, wave, records);

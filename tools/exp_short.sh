@@ -27,6 +27,14 @@ for v in "$@"; do
     ppt8) COP_PPT=8 step 200 "$out/bench20_ppt8.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 5 ;;
     relay16) COP_PMD_RELAY_STRIDE=16 step 200 "$out/bench20_relay16.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 ;;
     relay256) COP_PMD_RELAY_STRIDE=256 step 200 "$out/bench20_relay256.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 ;;
+    abrec) step 300 "$out/ab_rec_fw1k_L1024.log" python3 -u "$R/tools/ab.py" --workload fw1k --per-launch 1024 --rounds 7 --launches 4 base paired:COP_REC_PAIRED=1 base2 paired2:COP_REC_PAIRED=1 &&
+           step 300 "$out/ab_rec_fw_lpm_L1024.log" python3 -u "$R/tools/ab.py" --workload fw_lpm --per-launch 1024 --rounds 5 --launches 4 base paired:COP_REC_PAIRED=1 ;;
+    pairedtests) COP_REC_PAIRED=1 step 600 "$out/pytest_paired.log" python3 -u -m pytest "$R/tests/test_gpu_parity.py" "$R/tests/test_gpu_ring.py" "$R/tests/test_gpu_golden.py" "$R/tests/test_gpu_demux.py" -m gpu -x -q --timeout 300 --timeout-method thread ;;
+    abbase) step 300 "$out/ab_fw1k_L1024.log" python3 -u "$R/tools/ab.py" --workload fw1k --per-launch 1024 --rounds 7 --launches 4 base &&
+            step 300 "$out/ab_fw1k_L96.log" python3 -u "$R/tools/ab.py" --workload fw1k --per-launch 96 --rounds 7 --launches 8 base &&
+            step 300 "$out/ab_fw_lpm_L1024.log" python3 -u "$R/tools/ab.py" --workload fw_lpm --per-launch 1024 --rounds 5 --launches 4 base &&
+            step 300 "$out/ab_imix_L384.log" python3 -u "$R/tools/ab.py" --workload imix --per-launch 384 --rounds 5 --launches 4 base ;;
+    stamps) step 200 "$out/stamps_short.log" python3 -u "$R/tools/stamps.py" short ;;
     launch) step 200 "$out/bench20_launch.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 --engine launch ;;
   esac
 done
