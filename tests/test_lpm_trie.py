@@ -21,6 +21,8 @@ def probe_ips(tab, rng, n_random):
     (100000, cg.GEN_ROUTES, FORM_NH),     # the FW + LPM route table (BASELINE configs[2], [3])
     (1000, cg.GEN_FW, FORM_RULE),         # fw1k keyed by rule id
     (20000, cg.GEN_FW, FORM_NH),
+    (1000000, cg.GEN_ROUTES, FORM_NH),    # config 5's route table
+    (1000000, cg.GEN_FW, FORM_RULE),      # config 5's firewall, keyed by rule id
 ])
 def test_trie_equals_interval_search(n, kind, form):
     rules = cg.gen_rules(0x5EED7000 + n, n, kind, 0 if kind == cg.GEN_ROUTES else 20)
