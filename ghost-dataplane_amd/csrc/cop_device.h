@@ -416,6 +416,13 @@ struct Tables {
     uint32_t *fw_s, *fw_v, *lp_s, *lp_v;
 };
 
+// A random tbl24 probe: plain (cached) load, or non-temporal ($COP_PROBE_NT,
+// experiment: whether the streaming hint changes what a miss fetches)
+__device__ __forceinline__ uint32_t probe_ld(const uint32_t *a, uint32_t nt)
+{
+    return nt ? __builtin_nontemporal_load(a) : *a;
+}
+
 // Pass 1, per step: parse, vport route (stage P), interval searches in LDS,
 // and the tbl24 loads of DIR-24-8 stages (issued, not waited for).
 // w3 = bytes 12..15, w6/w7/w8 = bytes 24..35 of the packet as loaded (LE).
@@ -453,9 +460,9 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
         // lanes send no request); the others keep their stage-P verdict
         const bool reach = verdict[k] == COPK_FORWARD;
         if (FW == COPK_TBL_IVT) fwe[k] = t.fw_v[eyt_search(t.fw_s, fw_lv, src[k])];
-        if (FW == COPK_TBL_DIR) fwe[k] = reach ? p.fw_tbl24[src[k] >> 8] : 0u;
+        if (FW == COPK_TBL_DIR) fwe[k] = reach ? probe_ld(&p.fw_tbl24[src[k] >> 8], p.probe_nt) : 0u;
         if (LPM == COPK_TBL_IVT) lpe[k] = t.lp_v[eyt_search(t.lp_s, lp_lv, dst[k])];
-        if (LPM == COPK_TBL_DIR) lpe[k] = reach ? p.lpm_tbl24[dst[k] >> 8] : 0u;
+        if (LPM == COPK_TBL_DIR) lpe[k] = reach ? probe_ld(&p.lpm_tbl24[dst[k] >> 8], p.probe_nt) : 0u;
         if (LPM == COPK_TBL_TRIE) lpe[k] = t.lp_s[dst[k] >> 20];
     }
 }

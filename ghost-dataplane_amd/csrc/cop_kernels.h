@@ -97,6 +97,7 @@ struct CopKParams {
     const uint32_t *lpm_starts, *lpm_vals;
     const uint32_t *lpm_tbl24, *lpm_tbl8;
     uint32_t lpm_tbl8_packed;
+    uint32_t probe_nt;           // tbl24 probes as non-temporal loads (experiment, $COP_PROBE_NT)
     const uint32_t *lpm_tl0;     // trie form (lpm_trie.c): 4096 top entries (staged in LDS)
     const uint32_t *lpm_tnodes;  // 6 u32 per node: vec, leafvec (u64 each), child_base, leaf_base
     const uint32_t *lpm_tleaves;

@@ -179,6 +179,7 @@ struct cop_ctx {
     bool hit_bins = true;      // per-rule hit counters by binning ($COP_HIT_BINS=0: one atomic per hit)
     bool static_small = true;  // small launches in blockIdx tile order ($COP_STATIC_ORDER=0: tickets)
     bool rec_paired = false;   // one-shot kernel: records as 16-byte stores from lane pairs ($COP_REC_PAIRED=1)
+    bool probe_nt = false;     // tbl24 probes as non-temporal loads ($COP_PROBE_NT=1, experiment)
     uint32_t dbg = 0;          // $COP_DBG: timing-only kernel ablations
     uint32_t lds_pad = 0;      // $COP_LDS_PAD: extra LDS bytes per workgroup (occupancy experiments)
     unsigned long long *stamps = nullptr;   // dbg bit 8: per-workgroup phase stamps
@@ -486,6 +487,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_HIT_BINS")) c->hit_bins = atoi(e) != 0;
     if (const char *e = getenv("COP_STATIC_ORDER")) c->static_small = atoi(e) != 0;
     if (const char *e = getenv("COP_REC_PAIRED")) c->rec_paired = atoi(e) != 0;
+    if (const char *e = getenv("COP_PROBE_NT")) c->probe_nt = atoi(e) != 0;
     // route-table form for tables too large for LDS (A/B runs): trie | dir
     if (const char *e = getenv("COP_LPM_FORM")) {
         if (!strcmp(e, "trie")) c->cfg.flags |= COP_CFG_LPM_TRIE;
@@ -858,6 +860,7 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     p.lpm_tbl24 = c->lpm.tbl24;
     p.lpm_tbl8 = c->lpm.tbl8;
     p.lpm_tbl8_packed = c->lpm.tbl8_packed ? 1u : 0u;
+    p.probe_nt = c->probe_nt ? 1u : 0u;
     p.lpm_tl0 = c->lpm.tl0;
     p.lpm_tnodes = c->lpm.tnodes;
     p.lpm_tleaves = c->lpm.tleaves;

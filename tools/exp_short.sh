@@ -35,6 +35,9 @@ for v in "$@"; do
             step 300 "$out/ab_fw_lpm_L1024.log" python3 -u "$R/tools/ab.py" --workload fw_lpm --per-launch 1024 --rounds 5 --launches 4 base &&
             step 300 "$out/ab_imix_L384.log" python3 -u "$R/tools/ab.py" --workload imix --per-launch 384 --rounds 5 --launches 4 base ;;
     stamps) step 200 "$out/stamps_short.log" python3 -u "$R/tools/stamps.py" short ;;
+    abnt) step 300 "$out/ab_nt_fw_lpm_L1024.log" python3 -u "$R/tools/ab.py" --workload fw_lpm --per-launch 1024 --rounds 5 --launches 4 base nt:COP_PROBE_NT=1 &&
+          step 300 "$out/ab_nt_fw_lpm_1m_L25.log" python3 -u "$R/tools/ab.py" --workload fw_lpm_1m --per-launch 25 --rounds 5 --launches 8 base nt:COP_PROBE_NT=1 &&
+          step 300 "$out/ab_nt_imix_L384.log" python3 -u "$R/tools/ab.py" --workload imix --per-launch 384 --rounds 5 --launches 4 base nt:COP_PROBE_NT=1 ;;
     launch) step 200 "$out/bench20_launch.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 --engine launch ;;
   esac
 done
