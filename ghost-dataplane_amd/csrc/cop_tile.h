@@ -198,11 +198,28 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
     const uint32_t last = B.n ? B.n - 1 : 0u;
     if (LAY == COPK_LAY_COALESCED && B.n) {
         const StepGeom sg = step_geom(lane);
+#if defined(COPK_STREAM_W) && COPK_STREAM_W > 0
+        // experiment builds: a window of W steps in flight; step k + W is
+        // loaded into step k's registers once step k is gathered
+        constexpr int W = COPK_STREAM_W < PPT ? COPK_STREAM_W : PPT;
+        u32x4 v[W][3];
+#pragma unroll
+        for (int k = 0; k < W; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            gather_step(sg, v[k % W], w3[k], w6[k], w7[k], w8[k]);
+            if (k + W < PPT) {
+                __builtin_amdgcn_sched_barrier(0);
+                load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W]);
+            }
+        }
+#else
         u32x4 v[PPT][3];
 #pragma unroll
         for (int k = 0; k < PPT; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
 #pragma unroll
         for (int k = 0; k < PPT; k++) gather_step(sg, v[k], w3[k], w6[k], w7[k], w8[k]);
+#endif
     } else if (LAY == COPK_LAY_HDR16 && B.n) {
         // one 16-byte record per packet: frame bytes 12..15 then 24..35
 #pragma unroll

@@ -38,6 +38,14 @@ for v in "$@"; do
     abnt) step 300 "$out/ab_nt_fw_lpm_L1024.log" python3 -u "$R/tools/ab.py" --workload fw_lpm --per-launch 1024 --rounds 5 --launches 4 base nt:COP_PROBE_NT=1 &&
           step 300 "$out/ab_nt_fw_lpm_1m_L25.log" python3 -u "$R/tools/ab.py" --workload fw_lpm_1m --per-launch 25 --rounds 5 --launches 8 base nt:COP_PROBE_NT=1 &&
           step 300 "$out/ab_nt_imix_L384.log" python3 -u "$R/tools/ab.py" --workload imix --per-launch 384 --rounds 5 --launches 4 base nt:COP_PROBE_NT=1 ;;
+    abstream) for rep in 1 2; do for L in base w2 w4 w2e6; do
+                 if [ $L = base ]; then lib=libcopgpu.so; else lib=libcopgpu_$L.so; fi
+                 COP_LIB=$R/ghost-dataplane_amd/$lib step 200 "$out/ab_stream_${L}_fw1k_$rep.log" python3 -u "$R/tools/ab.py" --workload fw1k --per-launch 1024 --rounds 3 --launches 4 $L || exit 99
+               done; done
+               for L in base w2 w4 w2e6; do
+                 if [ $L = base ]; then lib=libcopgpu.so; else lib=libcopgpu_$L.so; fi
+                 COP_LIB=$R/ghost-dataplane_amd/$lib step 200 "$out/ab_stream_${L}_fw_lpm.log" python3 -u "$R/tools/ab.py" --workload fw_lpm --per-launch 1024 --rounds 3 --launches 4 $L || exit 99
+               done ;;
     launch) step 200 "$out/bench20_launch.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 --engine launch ;;
   esac
 done
