@@ -124,6 +124,41 @@ def check_devices(args, world, local, ndev):
                          f"own GPU (--allow-shared-gpu to time ranks sharing GPUs anyway)")
 
 
+def table_probes(fw_tab, rt_tab, sample, imix_offsets, route_form):
+    """SURVEY.md §8(d): LPM table probes are not in the algorithmic bytes;
+    report them per packet, from a sample batch of the workload (host-side
+    restatement of which packets reach each stage). LDS forms issue no
+    global-memory probe; DIR-24-8 issues one tbl24 load per packet that
+    reaches the stage and a tbl8 load when the entry is extended; the trie
+    form 2-4 node loads and a leaf load (L2-resident)."""
+    if imix_offsets is not None:
+        hdr = np.stack([sample[o:o + 36] for o in imix_offsets[:65536]])
+    else:
+        hdr = sample.reshape(-1, 64)[:, :36]
+    et = (hdr[:, 12].astype(np.uint32) << 8) | hdr[:, 13]
+    be = lambda c: ((hdr[:, c].astype(np.uint32) << 24) | (hdr[:, c + 1].astype(np.uint32) << 16)  # noqa: E731
+                    | (hdr[:, c + 2].astype(np.uint32) << 8) | hdr[:, c + 3])
+    src, dst = be(26), be(30)
+    reach = (et == 0x0800) & ((dst & 0xFFFF) > 4)   # stage P: the default routing table's UNKNOWN entries
+    n = len(hdr)
+    out = {"sample_pkts": int(n), "reach_stage_p": round(float(reach.mean()), 4)}
+    for name, tab, key, form in (("fw", fw_tab, src, "dir"), ("route", rt_tab, dst, route_form)):
+        if tab is None:
+            continue
+        if len(tab.intervals()[0]) <= 8192:
+            out[name] = {"form": "lds-intervals", "global_probes_per_pkt": 0.0}
+            continue
+        if form == "trie":
+            out[name] = {"form": "trie (LDS top level, L2 nodes)", "global_probes_per_pkt": None}
+            continue
+        t24, _ = tab.dir24()
+        e = t24[key[reach] >> 8]
+        ext = ((e & 0x03000000) == 0x03000000).sum()
+        out[name] = {"form": "dir24-8", "tbl24_per_pkt": round(float(reach.sum()) / n, 4),
+                     "tbl8_per_pkt": round(float(ext) / n, 4)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -196,8 +231,10 @@ def main():
         # RCCL communicator over the GPUs of the job (xGMI); id from rank 0 over gloo
         uid = group.broadcast_bytes(cg.coll_unique_id() if rank == 0 else None)
         ctx.coll_init(uid, rank, world)
+    rt_tab = None
     if routes is not None:
-        ctx.set_route_lpm(cg.LpmTable(routes, max(W["routes"], 1), 1 << 20, False))
+        rt_tab = cg.LpmTable(routes, max(W["routes"], 1), 1 << 20, False)
+        ctx.set_route_lpm(rt_tab)
     log(f"[rank {rank}] tables ready in {time.time() - t0:.1f}s on device {dev}")
 
     # ---- input pool: distinct batches, > Infinity Cache ----
@@ -490,6 +527,15 @@ def main():
         "cpu_baseline": None,
     }
     out["single_batch_latency"] = single_batch
+    try:   # a report only: never fails the line
+        if W["imix"]:
+            probes = table_probes(fw_tab, rt_tab, slab, offs, args.route_form)
+        else:
+            sample = cg.gen_trace(copdist.shard_seed(0x5EED0000 + cid, rank, 0), B, fw_rules, routes)
+            probes = table_probes(fw_tab, rt_tab, sample, None, args.route_form)
+        out["roofline"]["table_probes"] = probes
+    except Exception as e:  # noqa: BLE001
+        out["roofline"]["table_probes"] = {"error": repr(e)}
     if pmd_info:
         # the poll-mode kernel: a 1024-batch post (HBM-resident, one post, no
         # launch) timed on the host, as a fraction of the peak

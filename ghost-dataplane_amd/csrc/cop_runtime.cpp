@@ -720,7 +720,13 @@ int cop_set_fw_table(cop_ctx *c, const cop_lpm_table *t)
     if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel is serving this context (cop_pmd_stop first)");
     if (t->n_rules > COP_LPM_NH_MASK) return set_err(c, -EINVAL, "rule ids exceed 24 bits");
     int rc = upload_lpm(c, c->fw, t, !(c->cfg.flags & COP_CFG_FW_FORCE_DIR24), COP_FORM_RULE);
-    if (!rc && (c->cfg.flags & COP_CFG_RULE_COUNTERS)) rc = resize_counters(c, t->n_rules);
+    if (rc) {
+        // a failed upload leaves the stage with the empty table (every lookup
+        // misses), never with a partial image a launch could read
+        (void)upload_empty_ivt(c, c->fw);
+        return rc;
+    }
+    if (c->cfg.flags & COP_CFG_RULE_COUNTERS) rc = resize_counters(c, t->n_rules);
     return rc;
 }
 
@@ -728,8 +734,10 @@ int cop_set_route_lpm(cop_ctx *c, const cop_lpm_table *t)
 {
     if (!c || !t) return -EINVAL;
     if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel is serving this context (cop_pmd_stop first)");
-    return upload_lpm(c, c->lpm, t, !(c->cfg.flags & COP_CFG_LPM_FORCE_DIR24), COP_FORM_NH,
-                      (c->cfg.flags & COP_CFG_LPM_TRIE) != 0);
+    const int rc = upload_lpm(c, c->lpm, t, !(c->cfg.flags & COP_CFG_LPM_FORCE_DIR24), COP_FORM_NH,
+                              (c->cfg.flags & COP_CFG_LPM_TRIE) != 0);
+    if (rc) (void)upload_empty_ivt(c, c->lpm);   // as cop_set_fw_table
+    return rc;
 }
 
 int cop_load_fw_rules_file(cop_ctx *c, const char *path, const cop_lpm_config *cfg,
