@@ -46,6 +46,11 @@ for v in "$@"; do
                  if [ $L = base ]; then lib=libcopgpu.so; else lib=libcopgpu_$L.so; fi
                  COP_LIB=$R/ghost-dataplane_amd/$lib step 200 "$out/ab_stream_${L}_fw_lpm.log" python3 -u "$R/tools/ab.py" --workload fw_lpm --per-launch 1024 --rounds 3 --launches 4 $L || exit 99
                done ;;
+    fwlpm) step 300 "$out/bench_fw_lpm.log" python3 -u "$R/bench.py" --workload fw_lpm --steps 20 --warmup 5 --no-cpu --repeats 5 ;;
+    pf) COP_PMD_PREFETCH=1 step 200 "$out/bench20_pf.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 5 ;;
+    pfdefault) COP_PMD_PREFETCH=1 step 300 "$out/bench_default_pf.log" python3 -u "$R/bench.py" --engine pmd --no-cpu --repeats 3 &&
+               step 300 "$out/bench_default_pmd.log" python3 -u "$R/bench.py" --engine pmd --no-cpu --repeats 3 ;;
+    pftests) COP_PMD_PREFETCH=1 step 300 "$out/pytest_pmd_pf.log" python3 -u -m pytest "$R/tests/test_gpu_pmd.py" -m gpu -x -v --timeout 120 --timeout-method thread ;;
     launch) step 200 "$out/bench20_launch.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 --engine launch ;;
   esac
 done
