@@ -609,18 +609,27 @@ class Pmd:
         if not hasattr(ctx, "_pmds"):
             ctx._pmds = []
         ctx._pmds.append(self)
+        # bound once: these sit inside timed regions (a lookup per call costs
+        # a measurable part of a 30 us post)
+        L = lib()
+        self._post, self._wait, self._run = L.cop_pmd_post, L.cop_pmd_wait, L.cop_pmd_run
+        self._n_posted = 0   # every post goes through this object
 
     def post(self, count: int):
-        _check(lib().cop_pmd_post(self.handle, count), self.ctx, "pmd_post")
+        _check(self._post(self.handle, count), self.ctx, "pmd_post")
+        self._n_posted += count
 
     def wait(self, seq: int | None = None):
-        if seq is None:
-            seq = self.posted
-        _check(lib().cop_pmd_wait(self.handle, seq), self.ctx, "pmd_wait")
+        rc = self._wait(self.handle, self._n_posted if seq is None else seq)
+        if rc < 0:
+            _check(rc, self.ctx, "pmd_wait")
 
     def run(self, count: int):
         """Post `count` batches and wait for all of them (one C call)."""
-        _check(lib().cop_pmd_run(self.handle, count), self.ctx, "pmd_run")
+        rc = self._run(self.handle, count)
+        if rc < 0:
+            _check(rc, self.ctx, "pmd_run")
+        self._n_posted += count
 
     @property
     def posted(self) -> int:
