@@ -51,6 +51,7 @@ for v in "$@"; do
     pfdefault) COP_PMD_PREFETCH=1 step 300 "$out/bench_default_pf.log" python3 -u "$R/bench.py" --engine pmd --no-cpu --repeats 3 &&
                step 300 "$out/bench_default_pmd.log" python3 -u "$R/bench.py" --engine pmd --no-cpu --repeats 3 ;;
     pftests) COP_PMD_PREFETCH=1 step 300 "$out/pytest_pmd_pf.log" python3 -u -m pytest "$R/tests/test_gpu_pmd.py" -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    relayN) for st in 128 512 1280 256; do COP_PMD_RELAY_STRIDE=$st step 200 "$out/bench20_relay$st.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 || exit 99; done ;;
     launch) step 200 "$out/bench20_launch.log" python3 -u "$R/bench.py" --steps 20 --warmup 5 --no-cpu --repeats 21 --engine launch ;;
   esac
 done
