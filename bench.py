@@ -189,6 +189,9 @@ def main():
                     help="skip the untimed RCCL all-reduce of the ranks' counters at the end")
     ap.add_argument("--stages", type=int, default=0, help="ablation: override the workload's stage mask")
     ap.add_argument("--no-compact", action="store_true", help="ablation: no ordered forward lists")
+    ap.add_argument("--lists", default="seg", choices=("seg", "dense"),
+                    help="ordered forward lists: seg = 256-packet segments (COP_CFG_SEG_LISTS: per-segment "
+                         "lists + counts, no cross-tile prefix), dense = one list per batch (decoupled look-back)")
     ap.add_argument("--route-form", default="dir", choices=("dir", "trie"),
                     help="route tables too large for LDS: DIR-24-8 image (HBM / Infinity Cache) or the multibit "
                          "trie (12-bit LDS top level + L2-resident 6-bit nodes)")
@@ -225,7 +228,8 @@ def main():
         W = dict(W, stages=args.stages)
     ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32, n_streams=args.streams,
                      flags=(cg.CFG_RULE_COUNTERS if rc_on else 0) | (cg.CFG_NO_COMPACT if args.no_compact else 0)
-                     | (cg.CFG_LPM_TRIE if args.route_form == "trie" else 0))
+                     | (cg.CFG_LPM_TRIE if args.route_form == "trie" else 0)
+                     | (cg.CFG_SEG_LISTS if args.lists == "seg" else 0))
     ctx.set_fw_table(fw_tab)
     if rc_on:
         # RCCL communicator over the GPUs of the job (xGMI); id from rank 0 over gloo
@@ -252,7 +256,9 @@ def main():
     d_pkts = ctx.alloc(P * per_batch)
     d_res = ctx.alloc(P * B * 8)
     d_fwd = ctx.alloc(P * B * 4)
-    d_cnt = ctx.alloc(P * 4 + 16)
+    n_seg = (B + cg.SEG_PKTS - 1) // cg.SEG_PKTS
+    cnt_per_slot = n_seg if args.lists == "seg" else 1   # one count per segment, or per batch
+    d_cnt = ctx.alloc(P * cnt_per_slot * 4 + 16)
     if W["imix"]:
         # same packet mix in every batch slot, distinct addresses
         for i in range(P):
@@ -443,9 +449,10 @@ def main():
         log(f"[rank {rank}] rccl counter check: {allreduce_check}")
     fwd_frac = cnt["forward"] / max(1, cnt["rx"])
     # algorithmic bytes per packet: the 64 B header line (+4 B offset for
-    # IMIX), the 8 B result record, and 4 B per forwarded packet for the
-    # ordered forward list
-    bytes_per_pkt = (76 if W["imix"] else 72) + 4 * fwd_frac
+    # IMIX), the 8 B result record, 4 B per forwarded packet for the
+    # ordered forward list, and its counts (4 B per 256-packet segment, or
+    # per batch)
+    bytes_per_pkt = (76 if W["imix"] else 72) + 4 * fwd_frac + 4.0 * cnt_per_slot / B
     alg_bytes = bytes_per_pkt * B * Lb
     achieved = alg_bytes / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
 
@@ -496,6 +503,9 @@ def main():
             "pool_batches": int(P),
             "rule_counters": rc_on,
             "engine": args.engine,
+            "fwd_lists": ("none (ablation)" if args.no_compact else
+                          "segmented: per 256-packet segment an ordered list + count (COP_CFG_SEG_LISTS)"
+                          if args.lists == "seg" else "dense: one ordered list per batch (decoupled look-back)"),
             "ranks": ranks_info,
         },
         "roofline": {

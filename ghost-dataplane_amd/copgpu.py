@@ -24,7 +24,8 @@ FLAG_ROUTE_HIT, FLAG_FW_HIT = 0x1, 0x2
 COUNTER_SHARDS = 256   # COP_COUNTER_SHARDS
 LPM_STOP_AT_FIRST_ERROR = 0x1
 CFG_FW_FORCE_DIR24, CFG_LPM_FORCE_DIR24, CFG_NO_COMPACT, CFG_RULE_COUNTERS = 0x1, 0x2, 0x4, 0x8
-CFG_DEMUX_PORTS, CFG_PORT_STATS, CFG_LPM_TRIE = 0x10, 0x20, 0x40
+CFG_DEMUX_PORTS, CFG_PORT_STATS, CFG_LPM_TRIE, CFG_SEG_LISTS = 0x10, 0x20, 0x40, 0x80
+SEG_PKTS = 256   # COP_SEG_PKTS: packets per forward-list segment (CFG_SEG_LISTS)
 MAX_DEMUX_PORTS = 8
 GEN_FW, GEN_ROUTES = 0, 1
 UNKNOWN_PORT = 0xFFFF

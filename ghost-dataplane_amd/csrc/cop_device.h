@@ -165,9 +165,12 @@ __device__ __forceinline__ uint32_t eyt_search(const uint32_t *tree, uint32_t le
 // {epoch:32, flag:2 (1 aggregate, 2 inclusive), value:30}; a stale epoch
 // counts as not ready. Spins are bounded and report through the host-mapped
 // error word. Whole wave; returns the exclusive prefix.
+// exitw (poll-mode kernel: its exit word, else null): a wait that sees it set
+// gives up without publishing, since the predecessor it waits on may belong
+// to a worker that has left; the batch is redone whole after a relaunch.
 constexpr int LB_GROUPS = 4;
 __device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_t stride, uint32_t j, uint32_t agg,
-                                              uint32_t epoch, uint32_t *err, int lane)
+                                              uint32_t epoch, uint32_t *err, int lane, const uint32_t *exitw = nullptr)
 {
     const unsigned long long ep = (unsigned long long)epoch << 32;
     if (j == 0) {
@@ -215,6 +218,9 @@ __device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_
                 if (lane == 0) *err = 1u;
                 break;
             }
+            if (exitw && (spins & 63u) == 0 &&
+                __hip_atomic_load(exitw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                return excl;                  // the kernel is leaving: publish nothing
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -312,7 +318,9 @@ __device__ __forceinline__ CopKBatch batch_desc(const CopKParams &p, uint32_t b,
         B.offsets = p.rg.offsets ? p.rg.offsets + (size_t)slot * p.rg.offsets_slot_words : nullptr;
         B.results = (uint2 *)p.rg.results + (size_t)slot * p.rg.results_slot;
         B.fwd_idx = p.rg.fwd_idx ? p.rg.fwd_idx + (size_t)slot * p.rg.fwd_slot : nullptr;
-        B.fwd_count = p.rg.fwd_count ? p.rg.fwd_count + (size_t)slot * (p.demux ? p.demux : 1u) : nullptr;
+        // counts per slot: one, one per port (demux), or one per segment
+        const uint32_t per = p.seg ? (p.rg.n + COPK_SEG - 1u) / COPK_SEG : p.demux ? p.demux : 1u;
+        B.fwd_count = p.rg.fwd_count ? p.rg.fwd_count + (size_t)slot * per : nullptr;
         B.n = p.rg.n;
         B.stride = p.rg.stride;
         B.data_off = p.rg.data_off;
@@ -746,6 +754,7 @@ struct LookCtx {
     unsigned long long *look;
     uint32_t epoch;
     uint32_t *err;
+    const uint32_t *exitw = nullptr;   // poll-mode kernel: its exit word (look_back)
 };
 
 // LDS scratch of one compaction: per-(step, wave) counts and the prefix of
@@ -772,9 +781,58 @@ template <int PPT, bool WT, typename Mid>
 __device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, const CopKBatch &B, uint32_t lb_off,
                                              uint32_t j,
                                              uint32_t base, const bool (&fwd)[PPT], const uint32_t (&port)[PPT],
-                                             const CompactLds &s, int tid, int lane, int wave, Mid mid)
+                                             bool seg, const CompactLds &s, int tid, int lane, int wave, Mid mid)
 {
     constexpr int NQ = PPT * WAVES;
+    if (seg) {
+        // Segmented lists (COP_CFG_SEG_LISTS): step k of the tile is segment
+        // base/COPK_SEG + k, whose list is written at fwd_idx[(base + k*BLOCK) ..]
+        // and its length at fwd_count[segment]. Ballots and an LDS scan over
+        // the step's four waves order it; no other tile is involved.
+        static_assert(COPK_SEG == BLOCK, "one segment per tile step");
+        unsigned long long bal[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            bal[k] = __ballot(fwd[k]);
+            if (lane == 0) s.cnt[k * WAVES + wave] = (uint32_t)__popcll(bal[k]);
+        }
+        lds_barrier();
+        if (B.fwd_idx && !(o.dbg & 64u)) {
+#pragma unroll
+            for (int k = 0; k < PPT; k++) {
+                uint32_t off = 0;
+#pragma unroll
+                for (int w = 0; w < WAVES; w++) off += w < wave ? s.cnt[k * WAVES + w] : 0u;
+                if (fwd[k])
+                    s.stage[k * BLOCK + off +
+                            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[k] >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u))] =
+                        base + k * BLOCK + tid;
+            }
+        }
+        // the segments' lengths (segments holding packets of the batch only)
+        if (B.fwd_count && wave == 0 && lane < PPT && base + (uint32_t)lane * BLOCK < B.n) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int w = 0; w < WAVES; w++) c += s.cnt[lane * WAVES + w];
+            st_u32<WT>(c, B.fwd_count + base / COPK_SEG + (uint32_t)lane);
+        }
+        mid();
+        lds_barrier();
+        if (B.fwd_idx && !(o.dbg & 64u)) {
+            // 16-byte stores of each segment's first ceil(len/4) chunks
+            for (uint32_t q = (uint32_t)tid; q < (uint32_t)PPT * (BLOCK / 4); q += BLOCK) {
+                const uint32_t k = q / (BLOCK / 4), cc = q % (BLOCK / 4);
+                uint32_t c = 0;
+#pragma unroll
+                for (int w = 0; w < WAVES; w++) c += s.cnt[k * WAVES + w];
+                if (cc * 4u < c)
+                    st_u32x4<WT>(*(const u32x4 *)&s.stage[k * BLOCK + cc * 4u], B.fwd_idx,
+                                 (long)(base + k * BLOCK + cc * 4u));
+            }
+        }
+        return;
+    }
     if (!o.demux) {
         unsigned long long bal[PPT];
 #pragma unroll
@@ -802,7 +860,7 @@ __device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, co
         if (wave == 0) {
             // dbg bit 32 (timing-only ablation): no look-back wait, wrong offsets
             const uint32_t excl =
-                (o.dbg & 32u) ? j * 1024u : look_back(lk.look + lb_off, 1u, j, agg, lk.epoch, lk.err, lane);
+                (o.dbg & 32u) ? j * 1024u : look_back(lk.look + lb_off, 1u, j, agg, lk.epoch, lk.err, lane, lk.exitw);
             if (lane == 0) {
                 *s.pref = excl;
                 if (B.fwd_count && j == B.ntiles - 1) st_u32<WT>(excl + agg, B.fwd_count);
@@ -838,7 +896,7 @@ __device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, co
         uint32_t agg;
         const uint32_t ex = wave_excl_scan(lane < NQ ? s.dq[q * NQ + lane] : 0u, NQ, lane, &agg);
         if (lane < NQ) s.dq[q * NQ + lane] = ex;
-        const uint32_t excl = look_back(lk.look + (size_t)lb_off * K + q, K, j, agg, lk.epoch, lk.err, lane);
+        const uint32_t excl = look_back(lk.look + (size_t)lb_off * K + q, K, j, agg, lk.epoch, lk.err, lane, lk.exitw);
         if (lane == 0) {
             s.dpref[q] = excl;
             if (B.fwd_count && j == B.ntiles - 1) st_u32<WT>(excl + agg, &B.fwd_count[q]);

@@ -80,6 +80,10 @@ struct CopKParams {
     uint32_t stages;
     uint32_t n_ports;
     uint32_t compact;
+    // forward lists in segments of COPK_SEG packets (COP_CFG_SEG_LISTS):
+    // segment k's forward indices at fwd_idx[k*COPK_SEG ..), its length at
+    // fwd_count[k]; no cross-tile prefix, so no tickets and no look-back
+    uint32_t seg;
     uint32_t static_order;    // tile j of a batch = its blockIdx order (small launches: no ticket atomics)
     uint32_t epoch;
     uint32_t dbg;             // timing-only ablations ($COP_DBG), 0 in production
@@ -131,6 +135,7 @@ struct CopKParams {
 };
 #define COPK_HIT_SHIFT 14            /* 16384 rules per bucket: the count kernel's LDS counters (64 KiB) */
 #define COPK_HIT_MAX_BUCKETS 256     /* 4M rules */
+#define COPK_SEG 256                 /* packets per forward-list segment (= COPK_BLOCK: one tile step) */
 
 // Poll-mode (persistent) kernel, cop_pmd.hip: n_work worker workgroups
 // serve a batch ring; every relay_stride-th one relays the host's doorbell.
@@ -139,17 +144,18 @@ struct CopKPmd {
                                          // options; k.uniform_ntiles = tiles per batch
     const unsigned long long *h_posted;  // host-mapped: batches posted (monotonic)
     const uint32_t *h_stop;              // host-mapped: non-zero = leave once idle
-    unsigned long long *h_done;          // host-mapped: [slot] = sequence + 1 of its last completed batch
+    // host-mapped completion: [slot * tiles_per_batch + j] = sequence + 1 of
+    // the last batch whose tile j completed in that slot (every output byte
+    // of the tile, and its counter adds, landed before the word is written)
+    unsigned long long *h_tiles;
     uint32_t *h_state;                   // host-mapped: [0] exit reason (COPK_PMD_*), [1] census
     unsigned long long *d_posted;        // device relays of *h_posted: COPK_PMD_RELAYS copies, 128 B apart
     uint32_t *d_ctl;                     // device: [0] exit (COPK_PMD_*), [1] census, [2] look-back timeout
-    unsigned long long *slot_tiles;      // per ring slot: tiles completed (monotonic)
     unsigned long long *stamps;          // diagnostic: s_memrealtime per worker phase (COP_PMD_STAMPS) or null
     unsigned long long seq0;             // first batch sequence this launch serves
+    unsigned long long idle_ticks;       // s_memrealtime ticks (100 MHz) without a post before leaving
     uint32_t n_work;                     // worker workgroups
     uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
-    uint32_t idle_ticks;                 // s_memrealtime ticks (100 MHz) without a post before leaving
-    uint32_t defer_ctr;                  // add a tile's counters after signalling it (0: before, $COP_PMD_DEFER_CTR=0)
 };
 #define COPK_PMD_RELAYS 8
 #define COPK_PMD_RUNNING 0u

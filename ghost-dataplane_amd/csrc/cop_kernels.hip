@@ -102,7 +102,8 @@ __global__ __launch_bounds__(BLOCK, EXT ? 4 : COPK_WAVES_PER_EU) void cop_pipeli
 
     // ---- tile index inside the batch: this batch's ticket counter (or the
     // static order when no look-back runs: p.compact == 0) ----
-    const bool dyn = p.compact != 0 && !(o.dbg & 2u) && !p.static_order;
+    // (segmented lists need no cross-tile order: static too)
+    const bool dyn = p.compact != 0 && !p.seg && !(o.dbg & 2u) && !p.static_order;
     unsigned long long tk = 0;
     if (dyn && tid == 0) tk = ticket_take(&p.tickets[b * 16]);
 
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(BLOCK, EXT ? 4 : COPK_WAVES_PER_EU) void cop_pipeli
     STAMP(1);
 
     tile_body<FW, LPM, LAY, PPT, EXT, false>(p, o, lc, B, look_off, j, LookCtx{p.look, p.epoch, p.err}, tid, lane,
-                                             wave, !dyn);
+                                             wave, !dyn, blockIdx.x);
 }
 
 template <int FW, int LPM, int LAY, int PPT>

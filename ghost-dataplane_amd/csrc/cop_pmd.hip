@@ -17,10 +17,11 @@
 //     start-up census checks).
 // A tile is the one-shot kernel's tile body (cop_tile.h) with write-through
 // (sc1) output stores; after it every wave drains its stores, and one lane
-// counts the tile for its slot; the slot's last tile writes the batch's
-// sequence + 1 into the host-mapped completion word. The look-back chain of
-// slot s is tagged with the batch sequence, so chains of successive batches
-// in one slot never mix. Tables are staged into LDS once per worker.
+// writes the batch's sequence + 1 into the tile's host-mapped completion
+// word. With dense forward lists the look-back chain of slot s is tagged with
+// the batch sequence, so chains of successive batches in one slot never mix;
+// segmented lists (COP_CFG_SEG_LISTS) need no chain at all. Tables are
+// staged into LDS once per worker.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -68,11 +69,15 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
     unsigned long long *relay = P.d_posted + (blockIdx.x % COPK_PMD_RELAYS) * 16;
     unsigned long long seen = 0, t_seen = __builtin_amdgcn_s_memrealtime();
     for (uint32_t spins = 0;; spins++) {
-        unsigned long long hp = __hip_atomic_load(relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // every load of a poll is issued before any is used: one round trip
+        // per poll, not one per load (a leader's PCIe read overlaps the rest)
+        const unsigned long long hp = __hip_atomic_load(relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t ex = ld_agent(&P.d_ctl[0]);
+        unsigned long long h = 0;
+        if (leader) h = __hip_atomic_load(P.h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (hp > b) return hp;
-        if (ld_agent(&P.d_ctl[0])) return 0;
+        if (ex) return 0;
         if (leader) {
-            const unsigned long long h = __hip_atomic_load(P.h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
             if (h > hp) {
                 for (int r = 0; r < COPK_PMD_RELAYS; r++) atomicMax(P.d_posted + r * 16, h);
@@ -186,29 +191,29 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
         uint32_t look_off;
         const CopKBatch B = batch_desc(p, slot, &look_off);
-        // counters are added after the tile is signalled (defer_ctr), unless
-        // the tile bins rule hits (their sort needs the counters' barrier)
-        const bool defer = P.defer_ctr && !(EXT && p.hit_region);
-        tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(p, o, lc, B, look_off, j,
-                                                LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2]}, tid_i, lane_i,
-                                                wave_i, false, defer);
-        // completion: every wave's stores (write-through) have landed, then
-        // one lane counts the tile; the slot's last tile signals the host
+        if (EXT && p.hit_region) {
+            // binned rule hits: the tile's bucket counts start at zero (the
+            // last tile's sort is done with them: the barrier below ordered it)
+            for (uint32_t i = (uint32_t)tid_i; i < p.hit_nb; i += BLOCK) lds[p.lds_hit_off + i] = 0u;
+            lds_barrier();
+        }
+        tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
+            p, o, lc, B, look_off, j, LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0]}, tid_i, lane_i,
+            wave_i, false, (size_t)slot * tpb + j);
+        // completion: every wave's stores (write-through) and counter adds
+        // have landed, then one lane marks the tile done in host memory; the
+        // host sees batch b complete when all of its tiles' words read b + 1
+        // (no device-side count: no returning atomic on the critical path)
         if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
         if (tid == 0) {
-            const unsigned long long old = atomicAdd(&P.slot_tiles[slot], 1ull);
-            if ((old + 1) % tpb == 0)
-                __hip_atomic_store(&P.h_done[slot], b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&P.h_tiles[(size_t)slot * tpb + j], b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (stamp) {
-                st_stamp(&stamp[3], __builtin_amdgcn_s_memrealtime());   // stores drained, tile counted
-                st_stamp(&stamp[5], (old + 1) % tpb == 0 ? 1ull : 0ull);
+                st_stamp(&stamp[3], __builtin_amdgcn_s_memrealtime());   // stores drained, tile marked
+                st_stamp(&stamp[5], j == tpb - 1 ? 1ull : 0ull);
             }
         }
-        // the tile's counters (reduced into LDS by tile_body, ordered by the
-        // barrier above); the next tile rewrites that LDS only after barriers
-        if (defer) flush_counters_add(p, o, lc.s_red, lc.s_ps, tid);
         // next tile: T += G
         j += rb;
         uint32_t db = qb;

@@ -235,7 +235,10 @@ struct cop_ctx {
     cop_pmd *pmd = nullptr;             // the poll-mode kernel serving this context, if any
     hipStream_t tele_stream = nullptr;  // cop_counters_snapshot
     uint64_t *tele_host = nullptr;
-    unsigned long long *tele_dev = nullptr;
+    unsigned long long *tele_dev = nullptr;   // exchange_words scratch
+    size_t tele_words = 0;
+    unsigned long long *ctr_snap = nullptr;   // cop_coll_reduce_counters(reset): exchanged words
+    size_t ctr_snap_words = 0;
 };
 
 static int set_err(cop_ctx *c, int code, const char *fmt, ...)
@@ -326,6 +329,7 @@ void cop_destroy(cop_ctx *c)
     if (c->stamps) (void)hipFree(c->stamps);
     if (c->counters) (void)hipFree(c->counters);
     if (c->ctr_sum) (void)hipFree(c->ctr_sum);
+    if (c->ctr_snap) (void)hipFree(c->ctr_snap);
     coll_destroy(c);
     if (c->h_err) (void)hipHostFree(c->h_err);
     if (c->t0) (void)hipEventDestroy(c->t0);
@@ -839,7 +843,7 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     // LDS carve (u32 words): rt_top 256 | leaves nleaf*128 | fw 2m | lpm 2m | misc | list stage
     const uint32_t misc_words =
         (p.demux || (c->cfg.flags & COP_CFG_PORT_STATS)) ? COPK_LDS_MISC_EXT_WORDS : COPK_LDS_MISC_WORDS;
-    const bool stage_list = p.compact && !p.demux && c->stage_lists;
+    const bool stage_list = p.compact && !p.demux && (c->stage_lists || p.seg);
     auto lds_need = [&](int fwm, int lpmm) {
         return (256u + c->rt_nleaf * 128u + (fwm == COPK_TBL_IVT ? 2u * c->fw.m : 0u) +
                 (lpmm == COPK_TBL_IVT ? 2u * c->lpm.m : lpmm == COPK_TBL_TRIE ? COPK_TRIE_L0 : 0u) + misc_words +
@@ -1001,7 +1005,7 @@ static int launch_on(cop_ctx *c, Lane &L, CopKParams &p, bool imix, Plan pl, uin
     if (p.hit_region && (e = copk_hit_count(&p, grid, COPK_BLOCK * (uint32_t)ppt, L.s)) != hipSuccess)
         return set_err(c, -EIO, "hit count launch: %s", hipGetErrorString(e));
     L.dirty[q ^ 1] = 0;
-    L.dirty[q] = (p.compact && !(c->dbg & 2u) && !p.static_order) ? nb_used : 0;
+    L.dirty[q] = (p.compact && !p.seg && !(c->dbg & 2u) && !p.static_order) ? nb_used : 0;
     L.parity = q ^ 1;
     if (c->timing) {
         HIPCHK(c, hipEventRecord(L.ev[L.ev_head][1], L.s));
@@ -1042,6 +1046,12 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb,
         if (b.fwd_idx || b.fwd_count) compact = true;
     }
     if (c->cfg.flags & COP_CFG_NO_COMPACT) compact = false;
+    // segmented lists: public submits only (the library's own host paths
+    // read one dense list per batch)
+    const bool seg = demux && compact && (c->cfg.flags & COP_CFG_SEG_LISTS);
+    if (seg && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) return set_err(c, -EINVAL, "SEG_LISTS with DEMUX_PORTS");
+    for (uint32_t i = 0; seg && i < nb; i++)
+        if ((uintptr_t)batches[i].fwd_idx & 15) return set_err(c, -EINVAL, "batch %u: fwd_idx not 16-byte aligned", i);
     uint32_t min_stride = 0xFFFFFFFFu;
     for (uint32_t i = 0; i < nb; i++)
         if (batches[i].n) min_stride = std::min(min_stride, batches[i].stride);
@@ -1071,9 +1081,20 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb,
     for (uint32_t i = 1; i < nb; i++)
         if (p.b[i].ntiles != p.b[0].ntiles) p.uniform_ntiles = 0;
     p.compact = compact ? 1u : 0u;
+    p.seg = seg ? 1u : 0u;
     p.stages = stages;
     p.demux = (demux && compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 0u;
     return launch_on(c, L, p, imix, pl, nb);
+}
+
+// COP_CFG_SEG_LISTS rings: no demux, 16-byte aligned segments
+static int check_seg_ring(cop_ctx *c, const cop_batch_ring *r, bool seg)
+{
+    if (!seg) return 0;
+    if (c->cfg.flags & COP_CFG_DEMUX_PORTS) return set_err(c, -EINVAL, "SEG_LISTS with DEMUX_PORTS");
+    if (r->fwd_idx && (((uintptr_t)r->fwd_idx & 15) || (r->fwd_slot & 3)))
+        return set_err(c, -EINVAL, "ring: segmented lists need a 16-byte aligned fwd_idx and fwd_slot %% 4 == 0");
+    return 0;
 }
 
 int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, uint32_t count)
@@ -1092,6 +1113,8 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     const uint32_t lists = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 1u;
     if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < (uint64_t)r->n * lists))
         return set_err(c, -EINVAL, "ring: slot sizes smaller than n (x ports with demux)");
+    const bool seg = compact && (c->cfg.flags & COP_CFG_SEG_LISTS);
+    if (int rc = check_seg_ring(c, r, seg)) return rc;
     const Plan pl = plan_launch(c, (uint64_t)r->n * count, imix, r->stride);
     const uint32_t tile = COPK_BLOCK * pl.ppt;
     const uint32_t tpb = r->n ? (r->n + tile - 1) / tile : 1;
@@ -1116,6 +1139,7 @@ int cop_submit_ring(cop_ctx *c, const cop_batch_ring *r, uint32_t first_slot, ui
     p.ntiles = tpb * count;
     p.uniform_ntiles = tpb;
     p.compact = compact ? 1u : 0u;
+    p.seg = seg ? 1u : 0u;
     p.stages = c->cfg.stages;
     p.demux = lists > 1 || (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? lists : 0u;
     Lane &L = c->lane[c->next_lane];
@@ -1399,17 +1423,51 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
     return 0;
 }
 
+static int pmd_hits_flush(cop_ctx *c);
+
+// Counter words [off, off + n) of the counter block into host memory `out`,
+// read — or atomically exchanged with 0 when reset — by a small kernel on
+// the telemetry stream. Safe while launches or a poll-mode kernel run: an
+// increment lands before the exchange (this read) or after it (the next),
+// none is lost or counted twice. Does not wait for submitted work.
+static int exchange_words(cop_ctx *c, size_t off, size_t n, uint64_t *out, int reset)
+{
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->tele_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->tele_stream, hipStreamNonBlocking));
+    if (c->tele_words < n) {
+        if (c->tele_dev) (void)hipFree(c->tele_dev);
+        c->tele_dev = nullptr;
+        c->tele_words = 0;
+        HIPCHK(c, hipMalloc(&c->tele_dev, n * 8));
+        c->tele_words = n;
+    }
+    for (size_t done = 0; done < n;) {
+        const uint32_t k = (uint32_t)std::min<size_t>(n - done, (size_t)1 << 30);
+        hipError_t e = copk_snapshot(c->counters + off + done, k, c->tele_dev + done, reset ? 1 : 0, c->tele_stream);
+        if (e != hipSuccess) return set_err(c, -EIO, "snapshot: %s", hipGetErrorString(e));
+        done += k;
+    }
+    HIPCHK(c, hipMemcpyAsync(out, c->tele_dev, n * 8, hipMemcpyDeviceToHost, c->tele_stream));
+    HIPCHK(c, hipStreamSynchronize(c->tele_stream));
+    return 0;
+}
+
 int cop_counters_read(cop_ctx *c, cop_counters *out, int reset)
 {
     if (!c || !out) return -EINVAL;
     if (int rc = sync_lanes(c)) return rc;
-    std::vector<uint64_t> sh((size_t)COPK_COUNTER_SHARDS * COP_N_COUNTERS);
-    HIPCHK(c, hipMemcpy(sh.data(), c->counters, sh.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> sh(SHARD_WORDS);
+    if (c->pmd) {
+        // the poll-mode kernel may be adding: read (and zero) atomically
+        if (int rc = exchange_words(c, 0, SHARD_WORDS, sh.data(), reset)) return rc;
+    } else {
+        HIPCHK(c, hipMemcpy(sh.data(), c->counters, sh.size() * 8, hipMemcpyDeviceToHost));
+        if (reset) HIPCHK(c, memset_sync(c->counters, 0, sh.size() * 8, c->stream));
+    }
     uint64_t sum[COP_N_COUNTERS] = {0};
     for (int s = 0; s < COPK_COUNTER_SHARDS; s++)
         for (int k = 0; k < COP_N_COUNTERS; k++) sum[k] += sh[(size_t)s * COP_N_COUNTERS + k];
     memcpy(out, sum, sizeof(cop_counters));
-    if (reset) HIPCHK(c, memset_sync(c->counters, 0, sh.size() * 8, c->stream));
     return 0;
 }
 
@@ -1446,30 +1504,26 @@ int cop_port_stats_read(cop_ctx *c, cop_port_stats *out, uint32_t n, int reset)
     if (n > c->cfg.n_ports) n = c->cfg.n_ports;
     if (int rc = sync_lanes(c)) return rc;
     std::vector<uint64_t> sh(PORT_WORDS);
-    HIPCHK(c, hipMemcpy(sh.data(), c->counters + SHARD_WORDS, PORT_WORDS * 8, hipMemcpyDeviceToHost));
+    if (c->pmd) {
+        if (int rc = exchange_words(c, SHARD_WORDS, PORT_WORDS, sh.data(), reset)) return rc;
+    } else {
+        HIPCHK(c, hipMemcpy(sh.data(), c->counters + SHARD_WORDS, PORT_WORDS * 8, hipMemcpyDeviceToHost));
+        if (reset) HIPCHK(c, memset_sync(c->counters + SHARD_WORDS, 0, PORT_WORDS * 8, c->stream));
+    }
     fold_ports(sh.data(), out, n);
-    if (reset) HIPCHK(c, memset_sync(c->counters + SHARD_WORDS, 0, PORT_WORDS * 8, c->stream));
     return (int)c->cfg.n_ports;
 }
 
-// Live read(-and-zero) while launches are in flight: a small kernel on a
-// separate stream exchanges every counter word with 0 (or loads it) and the
-// copy goes to pinned memory; an increment lands either before the exchange
-// (this snapshot) or after it (the next one), none is lost.
+// Live read(-and-zero) while launches are in flight or a poll-mode kernel
+// runs (exchange_words): the print_stats read-and-zero (switch.c:33-90).
 int cop_counters_snapshot(cop_ctx *c, cop_counters *total, cop_port_stats *ports, uint32_t n_ports, int reset)
 {
     if (!c || (n_ports && !ports)) return -EINVAL;
-    if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel holds the GPU (snapshot after cop_pmd_stop)");
-    HIPCHK(c, hipSetDevice(c->device));
-    if (!c->tele_stream) {
-        HIPCHK(c, hipStreamCreateWithFlags(&c->tele_stream, hipStreamNonBlocking));
+    if (!c->tele_host) {
+        HIPCHK(c, hipSetDevice(c->device));
         HIPCHK(c, hipHostMalloc(&c->tele_host, RULE_OFF * 8, hipHostMallocDefault));
-        HIPCHK(c, hipMalloc(&c->tele_dev, RULE_OFF * 8));
     }
-    hipError_t e = copk_snapshot(c->counters, (uint32_t)RULE_OFF, c->tele_dev, reset ? 1 : 0, c->tele_stream);
-    if (e != hipSuccess) return set_err(c, -EIO, "snapshot: %s", hipGetErrorString(e));
-    HIPCHK(c, hipMemcpyAsync(c->tele_host, c->tele_dev, RULE_OFF * 8, hipMemcpyDeviceToHost, c->tele_stream));
-    HIPCHK(c, hipStreamSynchronize(c->tele_stream));
+    if (int rc = exchange_words(c, 0, RULE_OFF, c->tele_host, reset)) return rc;
     if (total) fold_shards(c->tele_host, total);
     if (n_ports) {
         if (n_ports > c->cfg.n_ports) n_ports = c->cfg.n_ports;
@@ -1483,8 +1537,17 @@ int cop_rule_counters_read(cop_ctx *c, uint64_t *out, uint32_t cap, int reset)
     if (!c || (cap && !out)) return -EINVAL;
     if (!(c->cfg.flags & COP_CFG_RULE_COUNTERS)) return set_err(c, -EINVAL, "rule counters not enabled");
     if (int rc = sync_lanes(c)) return rc;
+    if (int rc = pmd_hits_flush(c)) return rc;   // poll mode: count the binned hits of completed batches
     unsigned long long *d = c->counters + RULE_OFF;
     const uint32_t k = cap < c->n_rule_ctr ? cap : c->n_rule_ctr;
+    if (c->pmd && reset) {
+        // read-and-zero of every rule word at once, beside the running kernel
+        std::vector<uint64_t> all(c->n_rule_ctr);
+        if (c->n_rule_ctr)
+            if (int rc = exchange_words(c, RULE_OFF, c->n_rule_ctr, all.data(), 1)) return rc;
+        if (k) memcpy(out, all.data(), (size_t)k * 8);
+        return (int)c->n_rule_ctr;
+    }
     if (k) HIPCHK(c, hipMemcpy(out, d, (size_t)k * 8, hipMemcpyDeviceToHost));
     if (reset && c->n_rule_ctr) HIPCHK(c, memset_sync(d, 0, (size_t)c->n_rule_ctr * 8, c->stream));
     return (int)c->n_rule_ctr;
@@ -1569,6 +1632,7 @@ int cop_coll_reduce_counters(cop_ctx *c, cop_counters *total, uint64_t *rule_hit
     if (!c || (cap && !rule_hits)) return -EINVAL;
     if (!c->comm) return set_err(c, -EINVAL, "cop_coll_init not called");
     if (int rc = sync_lanes(c)) return rc;
+    if (int rc = pmd_hits_flush(c)) return rc;
     const size_t shard_words = SHARD_WORDS;
     const size_t words = RULE_OFF + c->n_rule_ctr;
     if (c->ctr_sum_words < words) {
@@ -1578,10 +1642,25 @@ int cop_coll_reduce_counters(cop_ctx *c, cop_counters *total, uint64_t *rule_hit
         HIPCHK(c, hipMalloc(&c->ctr_sum, words * 8));
         c->ctr_sum_words = words;
     }
+    // reset: read-and-zero every word first (an atomic exchange, so adds of
+    // a poll-mode kernel running beside it land in this interval or the
+    // next), then reduce that snapshot
+    const unsigned long long *src = c->counters;
+    if (reset) {
+        if (c->ctr_snap_words < words) {
+            if (c->ctr_snap) (void)hipFree(c->ctr_snap);
+            c->ctr_snap = nullptr;
+            c->ctr_snap_words = 0;
+            HIPCHK(c, hipMalloc(&c->ctr_snap, words * 8));
+            c->ctr_snap_words = words;
+        }
+        hipError_t e = copk_snapshot(c->counters, (uint32_t)words, c->ctr_snap, 1, c->stream);
+        if (e != hipSuccess) return set_err(c, -EIO, "snapshot: %s", hipGetErrorString(e));
+        src = c->ctr_snap;
+    }
     // ranks hold the same rule table, so the per-rule ranges line up
-    ncclResult_t r = g_rccl.all_reduce(c->counters, c->ctr_sum, words, ncclUint64, ncclSum, c->comm, c->stream);
+    ncclResult_t r = g_rccl.all_reduce(src, c->ctr_sum, words, ncclUint64, ncclSum, c->comm, c->stream);
     if (r != ncclSuccess) return set_err(c, -EIO, "ncclAllReduce: %s", g_rccl.error_string(r));
-    if (reset) HIPCHK(c, hipMemsetAsync(c->counters, 0, words * 8, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (total) {
         std::vector<uint64_t> sh(shard_words);
@@ -1707,16 +1786,24 @@ struct cop_pmd {
     volatile uint64_t *h_posted = nullptr;
     volatile uint32_t *h_stop = nullptr;
     volatile uint32_t *h_state = nullptr;
-    volatile uint64_t *h_done = nullptr;
-    uint8_t *dev = nullptr;                 // device words: relay, ctl, slot tile counts, look-back
+    volatile uint64_t *h_tiles = nullptr;   // [slot * tpb + j]: sequence + 1 once tile j is complete
+    uint8_t *dev = nullptr;                 // device words: relays, ctl, look-back (dense lists)
     size_t dev_bytes = 0;
     uint64_t posted = 0, completed = 0;
+    uint32_t tile_cursor = 0;               // tiles of batch `completed` seen complete so far
     uint32_t n_slots = 0, tpb = 0, per_cu = 0;
     uint32_t launches = 0;
     bool live = false;                      // a launch may still be running
+    // per-rule hits by binning: tile (slot, j) parks its sorted hit ids in
+    // region slot*tpb + j; cop_hit_count adds them up on stream hs, over
+    // runs of completed batches, before their slots are posted again
+    bool bins = false;
+    hipStream_t hs = nullptr;
+    uint64_t counted = 0;                   // batches < counted have their count launched
+    uint64_t count_synced = 0;              // ... and completed
 };
 
-// device words: [8] d_ctl, [256 + 128 r] relay r, then the slot tile counts
+// device words: [8] d_ctl, [256 + 128 r] relay r, then the look-back chains
 constexpr size_t PMD_RELAY_OFF = 256;
 constexpr size_t PMD_CTL_BYTES = PMD_RELAY_OFF + 128 * COPK_PMD_RELAYS;
 
@@ -1724,9 +1811,14 @@ static int pmd_launch(cop_pmd *m, uint64_t seq0)
 {
     cop_ctx *c = m->c;
     HIPCHK(c, hipSetDevice(c->device));
-    // device control words (d_posted, d_ctl) restart at 0; the slot tile
-    // counts carry over (every served batch completed: multiples of tpb)
-    HIPCHK(c, hipMemsetAsync(m->dev, 0, PMD_CTL_BYTES, m->s));
+    // every device word restarts at zero: relays, exit and census words, and
+    // the look-back chains. A launch that left idle may have left a batch
+    // half done (a post raced the idle exit); that batch is redone whole by
+    // this launch, so none of its granules may survive (their epoch tags
+    // would match). Its tiles' completion words can: a tile marks itself
+    // only after every byte it wrote has landed, and the redo writes the
+    // same bytes.
+    HIPCHK(c, hipMemsetAsync(m->dev, 0, m->dev_bytes, m->s));
     m->h_state[0] = 0;
     m->h_state[1] = 0;
     *m->h_stop = 0;
@@ -1757,27 +1849,57 @@ static int pmd_join(cop_pmd *m, double timeout_s)
     return 0;
 }
 
-// advance m->completed over the slots' completion words
+// advance m->completed over the tiles' completion words: batch b (slot
+// b % n_slots) is complete when all its tiles' words read b + 1
 static void pmd_refresh(cop_pmd *m)
 {
-    while (m->completed < m->posted && m->h_done[m->completed % m->n_slots] == m->completed + 1) m->completed++;
+    while (m->completed < m->posted) {
+        const uint64_t want = m->completed + 1;
+        const volatile uint64_t *t = m->h_tiles + (size_t)(m->completed % m->n_slots) * m->tpb;
+        while (m->tile_cursor < m->tpb && t[m->tile_cursor] == want) m->tile_cursor++;
+        if (m->tile_cursor < m->tpb) return;
+        m->completed++;
+        m->tile_cursor = 0;
+    }
 }
 
-static int pmd_census(cop_pmd *m);
-
-// the kernel left: relaunch after an idle exit (every batch it saw is
-// complete; posts it never saw start the new launch), else fail
-static int pmd_revive(cop_pmd *m)
+// count the binned rule hits of every completed batch not yet counted
+// (cop_hit_count over runs of consecutive slots, on stream hs, beside the
+// running kernel)
+static int pmd_hits_launch(cop_pmd *m)
 {
-    const uint32_t why = m->h_state[0];
-    if (why == COPK_PMD_RUNNING) return 0;
-    if (why != COPK_PMD_IDLE) return set_err(m->c, -EIO, "pmd kernel left (%s)", why == COPK_PMD_ABORT ?
-                                             "abort: workers not co-resident, or a look-back timed out" : "stopped");
-    if (int rc = pmd_join(m, 10.0)) return rc;
+    if (!m->bins) return 0;
+    const CopKParams &p = m->P.k;
+    while (m->counted < m->completed) {
+        const uint32_t s0 = (uint32_t)(m->counted % m->n_slots);
+        const uint32_t k = (uint32_t)std::min<uint64_t>(m->completed - m->counted, m->n_slots - s0);
+        CopKParams q = p;
+        q.hit_region = p.hit_region + (size_t)s0 * m->tpb * p.hit_reg_words;
+        q.hit_off = p.hit_off + (size_t)s0 * m->tpb * (p.hit_nb + 1);
+        hipError_t e = copk_hit_count(&q, k * m->tpb, COPK_BLOCK * (uint32_t)m->ppt, m->hs);
+        if (e != hipSuccess) return set_err(m->c, -EIO, "pmd hit count: %s", hipGetErrorString(e));
+        m->counted += k;
+    }
+    return 0;
+}
+
+// batches < upto counted and their count kernels done (their slots may be
+// rewritten, their hits are in the rule counters)
+static int pmd_hits_sync(cop_pmd *m, uint64_t upto)
+{
+    if (!m->bins || m->count_synced >= upto) return 0;
+    if (int rc = pmd_hits_launch(m)) return rc;
+    HIPCHK(m->c, hipStreamSynchronize(m->hs));
+    m->count_synced = m->counted;
+    return 0;
+}
+
+static int pmd_hits_flush(cop_ctx *c)
+{
+    cop_pmd *m = c->pmd;
+    if (!m || !m->bins) return 0;
     pmd_refresh(m);
-    if (int rc = pmd_launch(m, m->completed)) return rc;
-    const int st = pmd_census(m);
-    return st == 0 ? 0 : st < 0 ? st : set_err(m->c, -EIO, "pmd: workers never co-resident on relaunch");
+    return pmd_hits_sync(m, m->completed);
 }
 
 // every worker must be resident at once (static tile order): all of the
@@ -1807,6 +1929,37 @@ static int pmd_census(cop_pmd *m)
     }
 }
 
+// Launch serving from seq0 with every worker resident: when the census finds
+// workers that could not become resident (another kernel, context or process
+// holds CUs, likely after an idle exit), retry with one worker fewer per CU.
+static int pmd_launch_resident(cop_pmd *m, uint64_t seq0)
+{
+    for (;;) {
+        if (int rc = pmd_launch(m, seq0)) return rc;
+        const int st = pmd_census(m);
+        if (st == 0) return 0;
+        if (st < 0) return st;
+        if (int rc = pmd_join(m, 10.0)) return rc;
+        if (m->per_cu <= 1) return set_err(m->c, -EIO, "pmd: workers never co-resident");
+        m->per_cu--;
+        pmd_size(m);
+    }
+}
+
+// the kernel left: relaunch after an idle exit (every batch it completed
+// stays complete; the rest, posted before or after the exit, are served by
+// the new launch from the first incomplete one), else fail
+static int pmd_revive(cop_pmd *m)
+{
+    const uint32_t why = m->h_state[0];
+    if (why == COPK_PMD_RUNNING) return 0;
+    if (why != COPK_PMD_IDLE) return set_err(m->c, -EIO, "pmd kernel left (%s)", why == COPK_PMD_ABORT ?
+                                             "abort: workers not co-resident, or a look-back timed out" : "stopped");
+    if (int rc = pmd_join(m, 10.0)) return rc;
+    pmd_refresh(m);
+    return pmd_launch_resident(m, m->completed);
+}
+
 int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
 {
     if (!c || !r || !out) return -EINVAL;
@@ -1822,6 +1975,8 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
     const uint32_t lists = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 1u;
     if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < (uint64_t)r->n * lists))
         return set_err(c, -EINVAL, "pmd: slot sizes smaller than n (x ports with demux)");
+    const bool seg = compact && (c->cfg.flags & COP_CFG_SEG_LISTS);
+    if (int rc = check_seg_ring(c, r, seg)) return rc;
     if (int rc = sync_lanes(c)) return rc;
 
     cop_pmd *m = new (std::nothrow) cop_pmd();
@@ -1859,6 +2014,7 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
     p.ntiles = m->tpb;
     p.uniform_ntiles = m->tpb;
     p.compact = compact ? 1u : 0u;
+    p.seg = seg ? 1u : 0u;
     p.stages = c->cfg.stages;
     p.demux = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 0u;
     int rc = 0;
@@ -1886,6 +2042,27 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
                 PMD_FAIL(set_err(c, -ENOMEM, "pmd: stamps"));
             p.dbg = 8;
         }
+        // per-rule hits by binning, as in the one-shot kernel: one region per
+        // (slot, tile), counted by cop_hit_count beside the running kernel
+        if (p.rule_hits && c->hit_bins) {
+            const uint32_t nb = (c->n_rule_ctr + (1u << COPK_HIT_SHIFT) - 1) >> COPK_HIT_SHIFT;
+            const uint32_t reg = COPK_BLOCK * (uint32_t)ppt + 4u * nb;
+            const uint32_t base = (m->lds_bytes / 4u + 3u) & ~3u;
+            const uint32_t words = ((3u * nb + 5u + 3u) & ~3u) + COPK_BLOCK * (uint32_t)ppt + reg;
+            if (nb >= 1 && nb <= COPK_HIT_MAX_BUCKETS && (base + words) * 4u <= 160u * 1024u) {
+                const size_t tiles = (size_t)m->n_slots * m->tpb;
+                if (hipMalloc(&p.hit_region, tiles * reg * 4) != hipSuccess ||
+                    hipMalloc(&p.hit_off, tiles * (nb + 1) * 4) != hipSuccess)
+                    PMD_FAIL(set_err(c, -ENOMEM, "pmd: hit regions"));
+                if (hipStreamCreateWithFlags(&m->hs, hipStreamNonBlocking) != hipSuccess)
+                    PMD_FAIL(set_err(c, -EIO, "pmd: hit stream"));
+                p.hit_nb = nb;
+                p.hit_reg_words = reg;
+                p.lds_hit_off = base;
+                m->lds_bytes = (base + words) * 4u;
+                m->bins = true;
+            }
+        }
         m->ext = (p.demux || p.port_stats || p.rule_hits || p.dbg) ? 1 : 0;
         int occ = 0;
         hipError_t e = copk_pmd_occupancy(m->fw_mode, m->lpm_mode, m->layout, ppt, m->ext, m->lds_bytes, &occ);
@@ -1896,14 +2073,21 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         // start-up census confirms, else one fewer per CU is tried
         occ = std::min(occ, 6);
         if (p.dbg) occ = std::min(occ, 4);   // the EXT diagnostic kernel holds more registers
+        // binned hits: leave room beside the workers for the count kernel
+        // (64 KiB of LDS and a workgroup per CU)
+        if (m->bins) occ = std::min(occ, 4);
         if (const char *env = getenv("COP_PMD_PER_CU")) occ = std::min(occ, std::max(1, atoi(env)));
         m->per_cu = (uint32_t)occ;
         pmd_size(m);
-        m->P.idle_ticks = 100000000u;   // 1 s at 100 MHz
-        m->P.defer_ctr = getenv("COP_PMD_DEFER_CTR") && !atoi(getenv("COP_PMD_DEFER_CTR")) ? 0u : 1u;
-        if (const char *env = getenv("COP_PMD_IDLE_MS")) m->P.idle_ticks = (uint32_t)strtoul(env, nullptr, 0) * 100000u;
-        // control block in mapped host memory
-        const size_t ctl_bytes = 64 + (size_t)m->n_slots * 8;
+        m->P.idle_ticks = 100000000ull;   // 1 s at 100 MHz
+        if (const char *env = getenv("COP_PMD_IDLE_MS")) {
+            // ms -> ticks in 64 bits, clamped to a day
+            const unsigned long long ms = std::min<unsigned long long>(strtoull(env, nullptr, 0), 86400000ull);
+            m->P.idle_ticks = std::max<unsigned long long>(ms, 1ull) * 100000ull;
+        }
+        // control block in mapped host memory: posted, stop, state, then one
+        // completion word per (slot, tile)
+        const size_t ctl_bytes = 64 + (size_t)m->n_slots * m->tpb * 8;
         HIPCHK(c, hipSetDevice(c->device));
         if (hipHostMalloc(&m->ctl, ctl_bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             PMD_FAIL(set_err(c, -ENOMEM, "pmd: host control block"));
@@ -1913,14 +2097,15 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         m->h_posted = (volatile uint64_t *)m->ctl;
         m->h_stop = (volatile uint32_t *)(m->ctl + 8);
         m->h_state = (volatile uint32_t *)(m->ctl + 16);
-        m->h_done = (volatile uint64_t *)(m->ctl + 64);
+        m->h_tiles = (volatile uint64_t *)(m->ctl + 64);
         m->P.h_posted = (const unsigned long long *)dctl;
         m->P.h_stop = (const uint32_t *)((uint8_t *)dctl + 8);
         m->P.h_state = (uint32_t *)((uint8_t *)dctl + 16);
-        m->P.h_done = (unsigned long long *)((uint8_t *)dctl + 64);
-        // device words: control and relays, slot tile counts, then look-back
-        const size_t look_off = (PMD_CTL_BYTES + (size_t)m->n_slots * 8 + 255) & ~(size_t)255;
-        const size_t look_words = (size_t)m->n_slots * m->tpb * (p.demux ? p.demux : 1u);
+        m->P.h_tiles = (unsigned long long *)((uint8_t *)dctl + 64);
+        // device words: control and relays, then the look-back chains (dense
+        // lists only)
+        const size_t look_off = (PMD_CTL_BYTES + 255) & ~(size_t)255;
+        const size_t look_words = (compact && !seg) ? (size_t)m->n_slots * m->tpb * (p.demux ? p.demux : 1u) : 0;
         m->dev_bytes = look_off + look_words * 8;
         if (getenv("COP_PMD_STAMPS")) {   // diagnostic phase stamps (cop_debug_pmd_stamps)
             if (hipMalloc(&m->P.stamps, ((size_t)m->P.n_work * 8 + 128) * 8) != hipSuccess)
@@ -1931,23 +2116,14 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         if (hipMalloc(&m->dev, m->dev_bytes) != hipSuccess) PMD_FAIL(set_err(c, -ENOMEM, "pmd: device words"));
         if (hipStreamCreateWithFlags(&m->s, hipStreamNonBlocking) != hipSuccess)
             PMD_FAIL(set_err(c, -EIO, "pmd: stream"));
-        if (memset_sync(m->dev, 0, m->dev_bytes, m->s) != hipSuccess) PMD_FAIL(set_err(c, -EIO, "pmd: memset"));
         m->P.d_posted = (unsigned long long *)(m->dev + PMD_RELAY_OFF);
         m->P.d_ctl = (uint32_t *)(m->dev + 8);
-        m->P.slot_tiles = (unsigned long long *)(m->dev + PMD_CTL_BYTES);
-        p.look = (unsigned long long *)(m->dev + look_off);
+        p.look = look_words ? (unsigned long long *)(m->dev + look_off) : nullptr;
         p.err = nullptr;   // the look-back reports through d_ctl[2] (LookCtx)
         p.epoch = 0;
-        // launch; if the census finds workers that could not become
-        // resident, retry with one workgroup fewer per CU
-        for (;;) {
-            if ((rc = pmd_launch(m, 0))) goto fail;
-            const int st = pmd_census(m);
-            if (st == 0) break;
-            if (st < 0 || m->per_cu <= 1) PMD_FAIL(st < 0 ? st : set_err(c, -EIO, "pmd: workers never co-resident"));
-            if ((rc = pmd_join(m, 10.0))) goto fail;
-            m->per_cu--;
-            pmd_size(m);
+        if ((rc = pmd_launch_resident(m, 0))) {
+            (void)pmd_join(m, 10.0);
+            goto fail;
         }
     }
 #undef PMD_FAIL
@@ -1957,6 +2133,9 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
 fail:
     if (m->P.stamps) (void)hipFree(m->P.stamps);
     if (m->P.k.stamps) (void)hipFree(m->P.k.stamps);
+    if (m->P.k.hit_region) (void)hipFree(m->P.k.hit_region);
+    if (m->P.k.hit_off) (void)hipFree(m->P.k.hit_off);
+    if (m->hs) (void)hipStreamDestroy(m->hs);
     if (m->s) (void)hipStreamDestroy(m->s);
     if (m->dev) (void)hipFree(m->dev);
     if (m->ctl) (void)hipHostFree(m->ctl);
@@ -1973,6 +2152,8 @@ int cop_pmd_post(cop_pmd *m, uint32_t count)
     const uint64_t need = m->posted + count;
     if (need - m->completed > m->n_slots)
         if (int rc = cop_pmd_wait(m, need - m->n_slots)) return rc;
+    if (need > m->n_slots)   // the reused slots' binned hits are counted first
+        if (int rc = pmd_hits_sync(m, need - m->n_slots)) return rc;
     if (int rc = pmd_revive(m)) return rc;
     std::atomic_thread_fence(std::memory_order_seq_cst);   // ring slots written before the doorbell
     *m->h_posted = need;
@@ -2001,7 +2182,7 @@ int cop_pmd_wait(cop_pmd *m, uint64_t seq)
                            (unsigned long long)m->completed);
     }
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    return 0;
+    return pmd_hits_launch(m);
 }
 
 uint64_t cop_pmd_posted(const cop_pmd *m) { return m ? m->posted : 0; }
@@ -2037,16 +2218,21 @@ int cop_pmd_stop(cop_pmd *m)
     if (!m) return -EINVAL;
     cop_ctx *c = m->c;
     int rc = cop_pmd_wait(m, m->posted);
+    if (!rc) rc = pmd_hits_sync(m, m->completed);
     *m->h_stop = 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     const int jrc = pmd_join(m, 10.0);
     if (!rc) rc = jrc;
+    if (m->hs) (void)hipStreamSynchronize(m->hs);
     if (!jrc) {
         if (m->s) (void)hipStreamDestroy(m->s);
+        if (m->hs) (void)hipStreamDestroy(m->hs);
         if (m->dev) (void)hipFree(m->dev);
         if (m->ctl) (void)hipHostFree(m->ctl);
         if (m->P.stamps) (void)hipFree(m->P.stamps);
         if (m->P.k.stamps) (void)hipFree(m->P.k.stamps);
+        if (m->P.k.hit_region) (void)hipFree(m->P.k.hit_region);
+        if (m->P.k.hit_off) (void)hipFree(m->P.k.hit_off);
     }   // else: the kernel may still touch them; leak rather than free under it
     if (c->pmd == m) c->pmd = nullptr;
     delete m;

@@ -114,8 +114,9 @@ __device__ __forceinline__ void hit_hist(const HitLds &h, const bool (&valid)[PP
 // After a barrier that follows hit_hist: scan the bucket counts (each run
 // padded to 4 ids), place every hit's rule id in its bucket's run, and write
 // the runs (16-byte stores) and their offsets to the tile's region.
-template <int PPT>
-__device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &h, int tid, int lane, int wave)
+template <int PPT, bool WT>
+__device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &h, int tid, int lane, int wave,
+                                             size_t tile)
 {
     const uint32_t nb = p.hit_nb;
     uint32_t total;
@@ -169,10 +170,10 @@ __device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &
         lds_barrier();
         total = h.off[nb];
     }
-    uint32_t *reg = p.hit_region + (size_t)blockIdx.x * p.hit_reg_words;
+    uint32_t *reg = p.hit_region + tile * p.hit_reg_words;
     for (uint32_t c4 = (uint32_t)tid; c4 < total / 4u; c4 += BLOCK)
-        __builtin_nontemporal_store(*(const u32x4 *)&h.ids[4 * c4], (u32x4 *)&reg[4 * c4]);
-    for (uint32_t q = (uint32_t)tid; q <= nb; q += BLOCK) p.hit_off[(size_t)blockIdx.x * (nb + 1) + q] = h.off[q];
+        st_u32x4<WT>(*(const u32x4 *)&h.ids[4 * c4], reg, 4 * (long)c4);
+    for (uint32_t q = (uint32_t)tid; q <= nb; q += BLOCK) st_u32<WT>(h.off[q], &p.hit_off[tile * (nb + 1) + q]);
 }
 
 // One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,
@@ -180,11 +181,13 @@ __device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &
 // counter flush. Shared by the one-shot kernel (one tile per workgroup)
 // and the poll-mode kernel (cop_pmd.hip: a persistent loop over tiles).
 // WT: write-through output stores (poll-mode). sync_tables: wait for the
-// LDS-DMA table staging after the header loads are issued.
+// LDS-DMA table staging after the header loads are issued. hit_tile: the
+// tile's binned-hit region index (one-shot: blockIdx; poll mode: its slot's
+// tile).
 template <int FW, int LPM, int LAY, int PPT, bool EXT, bool WT>
 __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, const LdsCarve &lc, const CopKBatch &B,
                                           uint32_t look_off, uint32_t j, const LookCtx &lk, int tid, int lane, int wave,
-                                          bool sync_tables, bool defer_ctr = false)
+                                          bool sync_tables, size_t hit_tile)
 {
     constexpr bool IMIX = LAY == COPK_LAY_IMIX;
     const Tables &tb = lc.tb;
@@ -290,7 +293,8 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
         if (paired) store_records_paired<PPT, WT>(B, base, tid, lane, wave, valid, verdict, flags, port, rnh, fwd, cn);
         else store_records<PPT, WT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn, rec_stage);
     };
-    if (p.compact) compact_tile<PPT, WT>(lk, o, B, look_off, j, base, fwd, port, lc.cl, tid, lane, wave, records);
+    if (p.compact)
+        compact_tile<PPT, WT>(lk, o, B, look_off, j, base, fwd, port, p.seg != 0, lc.cl, tid, lane, wave, records);
     else records();
     if (rec_stage) {
         // compact_tile's second barrier (or this one) orders the staged records
@@ -302,14 +306,9 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
     // ---- counters (one flush per workgroup) ----
     uint32_t prx[COPK_MAX_DEMUX_PORTS] = {}, ptx[COPK_MAX_DEMUX_PORTS] = {};
     if (o.port_stats) port_counts<PPT>(o.port_stats, valid, fwd, port, prx, ptx);
-    if (defer_ctr && !bins) {
-        // the caller adds them (flush_counters_add) after a barrier of its own
-        flush_counters_lds(o, cn, prx, ptx, lc.s_red, lc.s_ps, lane, wave);
-    } else {
-        flush_counters(p, o, cn, prx, ptx, lc.s_red, lc.s_ps, tid, lane, wave);
-        // (flush_counters' barrier has landed every hit_hist add)
-        if (bins) hit_sort_out<PPT>(p, hit_lds<PPT>(p, lc.s_misc - p.lds_misc_off), tid, lane, wave);
-    }
+    flush_counters(p, o, cn, prx, ptx, lc.s_red, lc.s_ps, tid, lane, wave);
+    // (flush_counters' barrier has landed every hit_hist add)
+    if (bins) hit_sort_out<PPT, WT>(p, hit_lds<PPT>(p, lc.s_misc - p.lds_misc_off), tid, lane, wave, hit_tile);
     STAMP(6);
 }
 

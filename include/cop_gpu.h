@@ -209,6 +209,19 @@ typedef struct cop_ctx cop_ctx;
  * (12-bit top level in LDS, popcount-compressed 6-bit nodes, a few MiB that
  * stay in L2) instead of the 64 MiB DIR-24-8 image. Results are identical. */
 #define COP_CFG_LPM_TRIE        0x40u
+/* Segmented forward lists: a batch's ordered forward list is kept in
+ * segments of COP_SEG_PKTS consecutive packets. Segment k (packets
+ * k*COP_SEG_PKTS ..) holds its forwarded packets' indices, in arrival order,
+ * at fwd_idx[k*COP_SEG_PKTS ..] and their number at fwd_count[k]; so
+ * fwd_count holds ceil(n / COP_SEG_PKTS) words per batch (ring: per slot, at
+ * fwd_count + slot*ceil(n/COP_SEG_PKTS)), and fwd_idx must be 16-byte
+ * aligned (ring: fwd_slot a multiple of 4). Walking the segments in order
+ * yields exactly the dense list — the tx side drains it segment by segment,
+ * as coprocessor() hands its forward buffer over per burst of PKT_BURST_SZ
+ * (switch.c:464-473). No tile waits for another's count, so the kernels
+ * need no cross-workgroup prefix. Not combinable with DEMUX_PORTS. */
+#define COP_CFG_SEG_LISTS       0x80u
+#define COP_SEG_PKTS            256u
 #define COP_MAX_DEMUX_PORTS     8
 
 typedef struct cop_config {
@@ -351,8 +364,12 @@ int  cop_host_batch_wait(cop_ctx *ctx, uint32_t slot, const cop_result **results
  * exactly those of cop_submit_ring. No launch per post: no launch latency,
  * no grid ramp, tables staged into LDS once.
  * While it runs, the context's tables cannot change (-EBUSY) and it holds
- * nearly every workgroup slot of the GPU (other launches on the context
- * still run, slowly). One per context. The kernel leaves by itself after 1 s
+ * most workgroup slots of the GPU (other launches on the context still run,
+ * beside it). Counters stay readable: cop_counters_read /
+ * cop_counters_snapshot / cop_rule_counters_read see every completed batch
+ * (a batch's counter adds land before its completion), and their reset is
+ * an atomic read-and-zero, so nothing is lost or counted twice while
+ * batches run. One per context. The kernel leaves by itself after 1 s
  * without a post ($COP_PMD_IDLE_MS) and is relaunched by the next post. */
 typedef struct cop_pmd cop_pmd;
 int cop_pmd_start(cop_ctx *ctx, const cop_batch_ring *ring, cop_pmd **out);

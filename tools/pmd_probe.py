@@ -24,17 +24,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--posts", default="1,20,64,128")
+    ap.add_argument("--lists", default="seg", choices=("seg", "dense"))
     args = ap.parse_args()
     fw = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
     B, P = 65536, 128
-    ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, max_batch=B)
+    ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, max_batch=B,
+                     flags=cg.CFG_SEG_LISTS if args.lists == "seg" else 0)
     ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
     dp = ctx.alloc(P * B * 64)
     for i in range(0, P, 16):
         dp.upload(cg.gen_trace(0x5EED0002 + i, 16 * B, fw, None), i * B * 64)
     dr = ctx.alloc(P * B * 8)
     df = ctx.alloc(P * B * 4)
-    dc = ctx.alloc(P * 4 + 16)
+    dc = ctx.alloc(P * (B // cg.SEG_PKTS) * 4 + 16)
     ring = cg.make_ring(dp, P, B, dr, B * 64, stride=64, fwd_idx=df, fwd_count=dc)
     m = ctx.pmd_start(ring)
     info = m.info()
