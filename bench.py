@@ -81,8 +81,12 @@ def box_ceiling(pkts_addr, n_slots, out_addr):
                    ctypes.POINTER(ctypes.c_float)]
     fn.restype = ctypes.c_int
     best, best_name = None, None
-    # grid-stride copy at 4/8/16 workgroups per CU; LDS-DMA rings at 2/3 per CU
-    for pattern, mults, name in ((0, (4, 8, 16), "grid-stride"), (1, (2, 3), "lds-dma ring")):
+    # grid-stride copy at 4/8/16 workgroups per CU (and with 4 loads in flight
+    # per lane); LDS-DMA rings 2 deep at 2/3 per CU, 4 deep at 1/2, 8 deep at 1
+    # (MI355X_MICROARCH.md: float4 copy 6.29 TB/s, nt LDS-DMA streams 6.5-6.8)
+    for pattern, mults, name in ((0, (4, 8, 16), "grid-stride"), (4, (2, 4, 8), "grid-stride x4 in flight"),
+                                 (1, (2, 3), "lds-dma ring"), (2, (1, 2), "lds-dma ring 4-deep"),
+                                 (3, (1,), "lds-dma ring 8-deep")):
         for m in mults:
             ms = ctypes.c_float(0.0)
             if fn(pkts_addr, n_slots, out_addr, pattern, m, 5, ctypes.byref(ms)) == 0 and ms.value > 0:

@@ -144,13 +144,15 @@ struct CopKPmd {
                                          // options; k.uniform_ntiles = tiles per batch
     const unsigned long long *h_posted;  // host-mapped: batches posted (monotonic)
     const uint32_t *h_stop;              // host-mapped: non-zero = leave once idle
-    // host-mapped completion: [slot * tiles_per_batch + j] = sequence + 1 of
-    // the last batch whose tile j completed in that slot (every output byte
-    // of the tile, and its counter adds, landed before the word is written)
-    unsigned long long *h_tiles;
+    // host-mapped completion: [slot] = sequence + 1 of its last completed
+    // batch, written by the slot's last tile (every output byte of the batch,
+    // and its counter adds, landed before)
+    unsigned long long *h_done;
     uint32_t *h_state;                   // host-mapped: [0] exit reason (COPK_PMD_*), [1] census
     unsigned long long *d_posted;        // device relays of *h_posted: COPK_PMD_RELAYS copies, 128 B apart
     uint32_t *d_ctl;                     // device: [0] exit (COPK_PMD_*), [1] census, [2] look-back timeout
+    unsigned long long *slot_tiles;      // per ring slot: tiles completed (multiples of tiles per batch
+                                         // between batches; zeroed at every launch)
     unsigned long long *stamps;          // diagnostic: s_memrealtime per worker phase (COP_PMD_STAMPS) or null
     unsigned long long seq0;             // first batch sequence this launch serves
     unsigned long long idle_ticks;       // s_memrealtime ticks (100 MHz) without a post before leaving

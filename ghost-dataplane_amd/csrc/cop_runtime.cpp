@@ -1786,11 +1786,10 @@ struct cop_pmd {
     volatile uint64_t *h_posted = nullptr;
     volatile uint32_t *h_stop = nullptr;
     volatile uint32_t *h_state = nullptr;
-    volatile uint64_t *h_tiles = nullptr;   // [slot * tpb + j]: sequence + 1 once tile j is complete
-    uint8_t *dev = nullptr;                 // device words: relays, ctl, look-back (dense lists)
+    volatile uint64_t *h_done = nullptr;    // [slot]: sequence + 1 of its last completed batch
+    uint8_t *dev = nullptr;                 // device words: relays, ctl, slot tile counts, look-back
     size_t dev_bytes = 0;
     uint64_t posted = 0, completed = 0;
-    uint32_t tile_cursor = 0;               // tiles of batch `completed` seen complete so far
     uint32_t n_slots = 0, tpb = 0, per_cu = 0;
     uint32_t launches = 0;
     bool live = false;                      // a launch may still be running
@@ -1803,7 +1802,8 @@ struct cop_pmd {
     uint64_t count_synced = 0;              // ... and completed
 };
 
-// device words: [8] d_ctl, [256 + 128 r] relay r, then the look-back chains
+// device words: [8] d_ctl, [256 + 128 r] relay r, then the slot tile counts,
+// then the look-back chains (dense lists)
 constexpr size_t PMD_RELAY_OFF = 256;
 constexpr size_t PMD_CTL_BYTES = PMD_RELAY_OFF + 128 * COPK_PMD_RELAYS;
 
@@ -1811,13 +1811,11 @@ static int pmd_launch(cop_pmd *m, uint64_t seq0)
 {
     cop_ctx *c = m->c;
     HIPCHK(c, hipSetDevice(c->device));
-    // every device word restarts at zero: relays, exit and census words, and
-    // the look-back chains. A launch that left idle may have left a batch
-    // half done (a post raced the idle exit); that batch is redone whole by
-    // this launch, so none of its granules may survive (their epoch tags
-    // would match). Its tiles' completion words can: a tile marks itself
-    // only after every byte it wrote has landed, and the redo writes the
-    // same bytes.
+    // every device word restarts at zero: relays, exit and census words,
+    // the slot tile counts and the look-back chains. A launch that left idle
+    // may have left a batch half done (a post raced the idle exit): that
+    // batch is redone whole by this launch, so neither its partial tile
+    // count nor its granules (whose epoch tags would match) may survive.
     HIPCHK(c, hipMemsetAsync(m->dev, 0, m->dev_bytes, m->s));
     m->h_state[0] = 0;
     m->h_state[1] = 0;
@@ -1849,18 +1847,10 @@ static int pmd_join(cop_pmd *m, double timeout_s)
     return 0;
 }
 
-// advance m->completed over the tiles' completion words: batch b (slot
-// b % n_slots) is complete when all its tiles' words read b + 1
+// advance m->completed over the slots' completion words
 static void pmd_refresh(cop_pmd *m)
 {
-    while (m->completed < m->posted) {
-        const uint64_t want = m->completed + 1;
-        const volatile uint64_t *t = m->h_tiles + (size_t)(m->completed % m->n_slots) * m->tpb;
-        while (m->tile_cursor < m->tpb && t[m->tile_cursor] == want) m->tile_cursor++;
-        if (m->tile_cursor < m->tpb) return;
-        m->completed++;
-        m->tile_cursor = 0;
-    }
+    while (m->completed < m->posted && m->h_done[m->completed % m->n_slots] == m->completed + 1) m->completed++;
 }
 
 // count the binned rule hits of every completed batch not yet counted
@@ -2086,8 +2076,8 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
             m->P.idle_ticks = std::max<unsigned long long>(ms, 1ull) * 100000ull;
         }
         // control block in mapped host memory: posted, stop, state, then one
-        // completion word per (slot, tile)
-        const size_t ctl_bytes = 64 + (size_t)m->n_slots * m->tpb * 8;
+        // completion word per slot
+        const size_t ctl_bytes = 64 + (size_t)m->n_slots * 8;
         HIPCHK(c, hipSetDevice(c->device));
         if (hipHostMalloc(&m->ctl, ctl_bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             PMD_FAIL(set_err(c, -ENOMEM, "pmd: host control block"));
@@ -2097,14 +2087,14 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         m->h_posted = (volatile uint64_t *)m->ctl;
         m->h_stop = (volatile uint32_t *)(m->ctl + 8);
         m->h_state = (volatile uint32_t *)(m->ctl + 16);
-        m->h_tiles = (volatile uint64_t *)(m->ctl + 64);
+        m->h_done = (volatile uint64_t *)(m->ctl + 64);
         m->P.h_posted = (const unsigned long long *)dctl;
         m->P.h_stop = (const uint32_t *)((uint8_t *)dctl + 8);
         m->P.h_state = (uint32_t *)((uint8_t *)dctl + 16);
-        m->P.h_tiles = (unsigned long long *)((uint8_t *)dctl + 64);
-        // device words: control and relays, then the look-back chains (dense
-        // lists only)
-        const size_t look_off = (PMD_CTL_BYTES + 255) & ~(size_t)255;
+        m->P.h_done = (unsigned long long *)((uint8_t *)dctl + 64);
+        // device words: control and relays, slot tile counts, then the
+        // look-back chains (dense lists only)
+        const size_t look_off = (PMD_CTL_BYTES + (size_t)m->n_slots * 8 + 255) & ~(size_t)255;
         const size_t look_words = (compact && !seg) ? (size_t)m->n_slots * m->tpb * (p.demux ? p.demux : 1u) : 0;
         m->dev_bytes = look_off + look_words * 8;
         if (getenv("COP_PMD_STAMPS")) {   // diagnostic phase stamps (cop_debug_pmd_stamps)
@@ -2118,6 +2108,7 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
             PMD_FAIL(set_err(c, -EIO, "pmd: stream"));
         m->P.d_posted = (unsigned long long *)(m->dev + PMD_RELAY_OFF);
         m->P.d_ctl = (uint32_t *)(m->dev + 8);
+        m->P.slot_tiles = (unsigned long long *)(m->dev + PMD_CTL_BYTES);
         p.look = look_words ? (unsigned long long *)(m->dev + look_off) : nullptr;
         p.err = nullptr;   // the look-back reports through d_ctl[2] (LookCtx)
         p.epoch = 0;

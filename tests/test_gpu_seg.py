@@ -211,12 +211,12 @@ def test_pmd_live_snapshots_sum_exactly(gpu_ctx_factory):
             k = 1 + (i * 5) % 7
             m.post(k)
             posted += k
-            snap = ctx.snapshot(reset=True)
+            snap, _ = ctx.snapshot(reset=True)
             rx_sum += snap["rx"]
             if i % 3 == 2:
                 hits_sum += ctx.rule_counters(reset=True)
         m.wait()
-        rx_sum += ctx.snapshot(reset=True)["rx"]
+        rx_sum += ctx.snapshot(reset=True)[0]["rx"]
         hits_sum += ctx.rule_counters(reset=True)
     assert rx_sum == posted * B
     want = np.zeros(o.n_rules, np.uint64)
