@@ -22,6 +22,11 @@ Also reported (rank 0):
                 on the context's stream around every launch), vs 8 TB/s;
                 box_ceiling: what the same box sustains for the same byte mix
                 with no classification (tools/ceiling.hip), same pool;
+                probe_ceiling / probe_bound: the same box's random-probe rate
+                into tables of the pipeline's tbl24 size, and the pipeline's
+                LPM probes per second against it (DIR-24-8 workloads);
+  secondary     the north-star workload (FW + LPM 100k, 64 B) timed the same
+                way in the same run, with its own roofline (fw1k runs);
   cpu_baseline  the oracle's restatement of the reference CPU coprocessor()
                 loop (oracle/cop_oracle.c), 1 pinned core, bounded sample.
 """
@@ -46,6 +51,7 @@ HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # counter words ahead of the per-rule ones in the RCCL reduction: the
 # COP_COUNTER_SHARDS x 16 counter shards, then as many port-stat shards
 SHARD_AND_PORT_WORDS = 2 * 16 * cg.COUNTER_SHARDS
+TRAFFIC_DIR = os.path.join(ROOT, "bench_traffic")   # PMC traffic summaries the line quotes (travel with the tree)
 
 S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
 # config_id follows BASELINE.json configs[] (1-based); seeds per SURVEY.md §8d
@@ -67,20 +73,29 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def box_ceiling(pkts_addr, n_slots, out_addr):
-    """(GB/s, pattern) of the 72 B/packet copy mix on this box (None if the tool is absent)."""
+def _ceiling_lib():
     import ctypes
 
     path = os.path.join(ROOT, "tools", "libceiling.so")
     if not os.path.exists(path):
         log("[bench] tools/libceiling.so not built: no box ceiling")
         return None
-    lib = ctypes.CDLL(path)
+    return ctypes.CDLL(path)
+
+
+def box_ceiling(pkts_addr, n_slots, out_addr):
+    """(GB/s, pattern, {pattern: GB/s}) of the 72 B/packet copy mix on this
+    box (None if the tool is absent)."""
+    import ctypes
+
+    lib = _ceiling_lib()
+    if lib is None:
+        return None
     fn = lib.ceiling_pattern
     fn.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                    ctypes.POINTER(ctypes.c_float)]
     fn.restype = ctypes.c_int
-    best, best_name = None, None
+    best, best_name, every = None, None, {}
     # grid-stride copy at 4/8/16 workgroups per CU (and with 4 loads in flight
     # per lane); LDS-DMA rings 2 deep at 2/3 per CU, 4 deep at 1/2, 8 deep at 1
     # (MI355X_MICROARCH.md: float4 copy 6.29 TB/s, nt LDS-DMA streams 6.5-6.8)
@@ -90,17 +105,45 @@ def box_ceiling(pkts_addr, n_slots, out_addr):
         for m in mults:
             ms = ctypes.c_float(0.0)
             if fn(pkts_addr, n_slots, out_addr, pattern, m, 5, ctypes.byref(ms)) == 0 and ms.value > 0:
+                every[f"{name} x{m}/CU"] = round(72.0 * n_slots / (ms.value * 1e-3) / 1e9, 1)
                 if best is None or ms.value < best:
                     best, best_name = ms.value, f"{name} x{m}/CU"
     if best is None:
         return None
-    return 72.0 * n_slots / (best * 1e-3) / 1e9, best_name
+    return 72.0 * n_slots / (best * 1e-3) / 1e9, best_name, every
+
+
+def probe_ceiling(ctx, tables):
+    """Gprobes/s of uniformly random dword loads into `tables` tables of 2^24
+    u32 (64 MiB, the pipeline's tbl24 size) on this box, 8 packets per lane
+    with all probes in flight (tools/probe_kernels.h), or None."""
+    import ctypes
+
+    lib = _ceiling_lib()
+    if lib is None:
+        return None
+    fn = lib.ceiling_probe
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                   ctypes.POINTER(ctypes.c_float)]
+    fn.restype = ctypes.c_int
+    bufs = [ctx.alloc(64 << 20) for _ in range(2)]
+    try:
+        for i, b in enumerate(bufs):
+            b.fill(0x11 * (i + 1))
+        g = ctypes.c_float(0.0)
+        rc = fn(bufs[0].addr, bufs[1].addr, 1 << 24, tables, 5, ctypes.byref(g))
+        return float(g.value) if rc == 0 else None
+    finally:
+        for b in bufs:
+            b.free()
 
 
 def spawn_ranks(n: int) -> int:
     """Run this script as n rank processes (one per GPU) and return their
     worst exit status. The parent makes no GPU call: the ranks inherit its
-    stdout, where rank 0 prints the JSON line."""
+    stdout, where rank 0 prints the JSON line. Every rank is watched at once:
+    the first that fails ends the others (they would otherwise sit in a
+    gloo rendezvous or barrier until its long timeout)."""
     with socket.socket() as s_:
         s_.bind(("127.0.0.1", 0))
         port = s_.getsockname()[1]
@@ -109,11 +152,31 @@ def spawn_ranks(n: int) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p_.wait() for p_ in procs]
-    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
-    if bad:
-        log(f"[bench] ranks failed (rank, exit status): {bad}")
-        return max(abs(rc) for _, rc in bad) or 1
+    rcs = [None] * n
+    bad = None
+    while any(rc is None for rc in rcs):
+        for r, p_ in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p_.poll()
+                if rcs[r] not in (None, 0) and bad is None:
+                    bad = r
+        if bad is not None:
+            for p_ in procs:
+                if p_.poll() is None:
+                    p_.terminate()
+            for r, p_ in enumerate(procs):
+                try:
+                    rcs[r] = p_.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p_.kill()
+                    rcs[r] = p_.wait()
+            break
+        time.sleep(0.05)
+    failed = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if failed:
+        log(f"[bench] ranks failed (rank, exit status): {failed}" + (f"; rank {bad} failed first" if bad is not None
+                                                                    else ""))
+        return max(abs(rc) for _, rc in failed) or 1
     return 0
 
 
@@ -163,60 +226,33 @@ def table_probes(fw_tab, rt_tab, sample, imix_offsets, route_form):
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--allow-shared-gpu", action="store_true",
-                    help="let more ranks than visible GPUs run (they share GPUs; the line says so)")
-    ap.add_argument("--dry-run", action="store_true",
-                    help="test the launch and rank protocol only: no GPU, fake timings (CPU tests)")
-    ap.add_argument("--dry-run-devices", type=int, default=8, help="GPUs a --dry-run pretends to see")
-    ap.add_argument("--steps", type=int, default=16384)
-    ap.add_argument("--warmup", type=int, default=2048)
-    ap.add_argument("--workload", default="fw1k", choices=sorted(WORKLOADS))
-    ap.add_argument("--per-launch", type=int, default=0,
-                    help="batches per kernel launch (ring submit, at most 1024; 0: the workload's default). The "
-                         "~23 us per-launch ramp and tail cost 6 %% at 384 batches, 2.5 %% at 1024")
-    ap.add_argument("--streams", type=int, default=1, help="launch lanes (concurrent streams)")
-    ap.add_argument("--engine", default="auto", choices=("auto", "pmd", "launch"),
-                    help="pmd: the poll-mode kernel serves the batch ring (steps are posted to it); launch: one "
-                         "kernel launch per --per-launch steps; auto: pmd for short runs (< 1024 steps: no "
-                         "per-launch ramp), launch for long runs (large launches stream faster) and whenever "
-                         "per-rule counters are on (their binned counting runs after each launch)")
-    ap.add_argument("--pool-mib", type=int, default=0,
-                    help="distinct input bytes per GPU (0: max(400 MiB, one launch of batches))")
-    ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the value is their median")
-    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-rule-counters", action="store_true", help="ablation: config 5 without per-rule counters")
-    ap.add_argument("--no-rccl-check", action="store_true",
-                    help="skip the untimed RCCL all-reduce of the ranks' counters at the end")
-    ap.add_argument("--stages", type=int, default=0, help="ablation: override the workload's stage mask")
-    ap.add_argument("--no-compact", action="store_true", help="ablation: no ordered forward lists")
-    ap.add_argument("--lists", default="seg", choices=("seg", "dense"),
-                    help="ordered forward lists: seg = 256-packet segments (COP_CFG_SEG_LISTS: per-segment "
-                         "lists + counts, no cross-tile prefix), dense = one list per batch (decoupled look-back)")
-    ap.add_argument("--route-form", default="dir", choices=("dir", "trie"),
-                    help="route tables too large for LDS: DIR-24-8 image (HBM / Infinity Cache) or the multibit "
-                         "trie (12-bit LDS top level + L2-resident 6-bit nodes)")
-    args = ap.parse_args()
+def dir_probes_per_pkt(probes) -> tuple:
+    """(random DIR-24-8 probes per packet, tbl24 tables probed)."""
+    total, tables = 0.0, 0
+    for k in ("fw", "route"):
+        d = probes.get(k) or {}
+        if d.get("form") == "dir24-8":
+            total += d["tbl24_per_pkt"] + d["tbl8_per_pkt"]
+            tables += 1
+    return total, tables
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus))
-    rank, world, local = copdist.env()
-    W = WORKLOADS[args.workload]
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def measure(args, name, rank, world, dev, group, primary):
+    """Time `args.steps` steps of workload `name` (+ its kernel roofline);
+    returns (result dict, context). The caller closes the context."""
+    W = WORKLOADS[name]
     B = W["batch"]
-    Lb = max(1, args.per_launch or W["per_launch"])
-
-    if args.dry_run:
-        return dry_run(args, rank, world, local, W)
-    cg.lib()   # load the HIP runtime the product links (before torch)
-    ndev = cg.device_count()
-    check_devices(args, world, local, ndev)
-    dev = copdist.device_for(local, ndev)
-    group = copdist.Group(rank, world, "gloo")
-
-    # ---- tables (identical on every rank; packets differ per rank) ----
+    Lb = max(1, (args.per_launch if primary else 0) or W["per_launch"])
     cid = W["cid"]
     t0 = time.time()
     fw_rules = cg.gen_rules(0x5EED1000 + cid, W["fw"], cg.GEN_FW, 20 if W["fw"] <= 1000 else 0)
@@ -226,27 +262,35 @@ def main():
     else:
         fw_tab = cg.LpmTable(fw_rules, W["fw"], 1 << 20, False)
     rc_on = bool(W.get("rule_counters")) and not args.no_rule_counters
-    if args.engine == "auto":
-        args.engine = "launch" if rc_on or args.steps >= 1024 else "pmd"
-    if args.stages:
-        W = dict(W, stages=args.stages)
-    ctx = cg.Context(device=dev, stages=W["stages"], max_batch=B, max_batches=32, n_streams=args.streams,
+    engine = args.engine
+    if engine == "auto":
+        # the poll-mode kernel for short runs (no per-launch ramp), one-shot
+        # launches of up to 1024 batches for long runs (they stream faster)
+        engine = "launch" if args.steps >= 1024 else "pmd"
+    stages = args.stages if (args.stages and primary) else W["stages"]
+    seg = args.lists == "seg"
+    ctx = cg.Context(device=dev, stages=stages, max_batch=B, max_batches=32, n_streams=args.streams,
                      flags=(cg.CFG_RULE_COUNTERS if rc_on else 0) | (cg.CFG_NO_COMPACT if args.no_compact else 0)
                      | (cg.CFG_LPM_TRIE if args.route_form == "trie" else 0)
-                     | (cg.CFG_SEG_LISTS if args.lists == "seg" else 0))
+                     | (cg.CFG_SEG_LISTS if seg else 0))
     ctx.set_fw_table(fw_tab)
+    coll = None
     if rc_on:
         # RCCL communicator over the GPUs of the job (xGMI); id from rank 0 over gloo
-        uid = group.broadcast_bytes(cg.coll_unique_id() if rank == 0 else None)
-        ctx.coll_init(uid, rank, world)
+        try:
+            uid = group.broadcast_bytes(cg.coll_unique_id() if rank == 0 else None)
+            ctx.coll_init(uid, rank, world)
+            coll = "ok"
+        except Exception as e:  # noqa: BLE001 (reported per rank; the reduce is then skipped)
+            coll = f"error: {str(e)[:120]}"
     rt_tab = None
     if routes is not None:
         rt_tab = cg.LpmTable(routes, max(W["routes"], 1), 1 << 20, False)
         ctx.set_route_lpm(rt_tab)
-    log(f"[rank {rank}] tables ready in {time.time() - t0:.1f}s on device {dev}")
+    log(f"[rank {rank}] {name}: tables ready in {time.time() - t0:.1f}s on device {dev}")
 
     # ---- input pool: distinct batches, > Infinity Cache ----
-    pool_bytes = args.pool_mib << 20
+    pool_bytes = (args.pool_mib << 20) if primary else 0
     t0 = time.time()
     if W["imix"]:
         slab, offs = cg.gen_imix(copdist.shard_seed(0x5EED0000 + cid, rank), B, fw_rules, routes)
@@ -261,7 +305,7 @@ def main():
     d_res = ctx.alloc(P * B * 8)
     d_fwd = ctx.alloc(P * B * 4)
     n_seg = (B + cg.SEG_PKTS - 1) // cg.SEG_PKTS
-    cnt_per_slot = n_seg if args.lists == "seg" else 1   # one count per segment, or per batch
+    cnt_per_slot = n_seg if seg else 1   # one count per segment, or per batch
     d_cnt = ctx.alloc(P * cnt_per_slot * 4 + 16)
     if W["imix"]:
         # same packet mix in every batch slot, distinct addresses
@@ -274,7 +318,8 @@ def main():
             k = min(chunk, P - i)
             pk = cg.gen_trace(copdist.shard_seed(0x5EED0000 + cid, rank, i), k * B, fw_rules, routes)
             d_pkts.upload(pk, i * per_batch)
-    log(f"[rank {rank}] pool: {P} batches x {B} pkts ({P * per_batch / 2**20:.0f} MiB) in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] {name}: pool {P} batches x {B} pkts ({P * per_batch / 2**20:.0f} MiB) in "
+        f"{time.time() - t0:.1f}s")
 
     # the pool is a batch ring in HBM: one launch = Lb consecutive slots
     Lb = min(Lb, P)
@@ -288,7 +333,7 @@ def main():
 
     def pmd_on():
         nonlocal pmd
-        if args.engine == "pmd" and pmd is None:
+        if engine == "pmd" and pmd is None:
             pmd = ctx.pmd_start(ring)
 
     def pmd_off():
@@ -312,16 +357,15 @@ def main():
             s += k
 
     def sync_all():
-        if pmd is not None:
-            pmd.wait()      # (run_steps has waited already; the lanes hold no work)
-        else:
+        if pmd is None:
             ctx.sync()
+        # (poll mode: run_steps waited for every posted batch already)
 
     # ---- warmup, then exactly K timed steps, `repeats` times; the value is
     # the median run (median of 5 runs) ----
     pmd_on()
     run_steps(0, args.warmup)
-    runs, own_runs = [], []
+    runs, own_runs, reduce_runs = [], [], []
     red_tot = None
     for r in range(max(1, args.repeats)):
         pmd_on()
@@ -330,13 +374,12 @@ def main():
         sync_all()
         t0 = time.perf_counter()
         run_steps(args.warmup + r * args.steps, args.steps)
-        if rc_on:
-            # one reporting interval: sum counters + per-rule hits over all
-            # GPUs (the RCCL kernels need the CUs the poll-mode kernel holds:
-            # it completes and stops first, inside the timing)
-            sync_all()
-            pmd_off()
+        if rc_on and coll == "ok":
+            # one reporting interval: read-and-zero the counters + per-rule
+            # hits and sum them over all GPUs (RCCL beside the running
+            # poll-mode kernel: an atomic exchange, then the all-reduce)
             tot, _ = ctx.coll_reduce_counters(reset=True, with_rules=False)
+            reduce_runs.append(int(tot["rx"]))
             if red_tot is None:
                 red_tot = tot   # the first interval also holds the warmup
         sync_all()
@@ -347,17 +390,21 @@ def main():
     elapsed = float(np.median(runs))
     total_pkts = world * args.steps * B
     value = total_pkts / elapsed / 1e6
-    # this rank's own rate (its own clock, not the max over ranks), and its device
     own_rate = args.steps * B / float(np.median(own_runs)) / 1e6
-    ranks_info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(own_rate, 3)})
-    log(f"[rank {rank}] timed {args.steps} steps x {len(runs)} runs ({args.engine}), median {elapsed * 1e3:.3f} ms "
-        f"-> {value:.1f} Mpkt/s (all ranks); runs {[round(x * 1e3, 3) for x in runs]} ms")
+    log(f"[rank {rank}] {name}: timed {args.steps} steps x {len(runs)} runs ({engine}), median "
+        f"{elapsed * 1e3:.3f} ms -> {value:.1f} Mpkt/s (all ranks); runs {[round(x * 1e3, 3) for x in runs]} ms")
+    res = {"W": W, "name": name, "B": B, "Lb": Lb, "P": P, "engine": engine, "value": value, "elapsed": elapsed,
+           "runs": runs, "own_rate": own_rate, "rc_on": rc_on, "coll": coll, "fw_rules": fw_rules, "routes": routes,
+           "fw_tab": fw_tab, "rt_tab": rt_tab, "cnt_per_slot": cnt_per_slot, "d_pkts": d_pkts, "d_res": d_res,
+           # every buffer the ring points at stays referenced as long as the
+           # ring is used (a DeviceBuffer frees its memory when collected)
+           "bufs": (d_pkts, d_res, d_fwd, d_cnt), "ring": ring, "per_batch": per_batch}
+    if W["imix"]:
+        res["slab"], res["offs"] = slab, offs
 
     # ---- the poll-mode kernel's steady state and single-batch latency ----
-    pmd_info = None
-    if args.engine == "pmd":
+    if engine == "pmd" and primary:
         pmd_on()
-        sync_all()
         n_long = min(P, 1024)
         longs = []
         for _ in range(3):
@@ -383,26 +430,30 @@ def main():
         t_one = time.perf_counter() - t0
         info = pmd.info()
         t_long = float(np.median(longs))
-        pmd_info = {"workers": info["workers"], "workers_per_cu": info["workers_per_cu"],
-                    "packets_per_tile": info["packets_per_tile"], "launches": info["launches"],
-                    "steady_batches": n_long, "steady_mpkt_s": round(n_long * B / t_long / 1e6, 3),
-                    "steady_ms": round(t_long * 1e3, 4),
-                    "single_batch_post_to_done_us_median": round(float(np.median(lat)), 2),
-                    "one_batch_posts": {"batches": n_one, "in_flight": depth,
-                                        "mpkt_s": round(n_one * B / t_one / 1e6, 3)}}
-        pmd_off()
+        res["pmd_info"] = {"workers": info["workers"], "workers_per_cu": info["workers_per_cu"],
+                           "packets_per_tile": info["packets_per_tile"], "launches": info["launches"],
+                           "steady_batches": n_long, "steady_mpkt_s": round(n_long * B / t_long / 1e6, 3),
+                           "steady_ms": round(t_long * 1e3, 4),
+                           "single_batch_post_to_done_us_median": round(float(np.median(lat)), 2),
+                           "one_batch_posts": {"batches": n_one, "in_flight": depth,
+                                               "mpkt_s": round(n_one * B / t_one / 1e6, 3)}}
+    pmd_off()
 
-    reduce_info = None
-    if rc_on:
-        # the reduction alone (counters are zero now: same bytes, same cost)
+    if rc_on and coll == "ok":
+        # the reduction alone (counters are zero now: same bytes, same cost);
+        # the interval sums are checked and reported, never asserted (one
+        # failing rank must not kill the whole N-GPU line)
         group.barrier()
         r0 = time.perf_counter()
         ctx.coll_reduce_counters(reset=False, with_rules=False)
         r_ms = (time.perf_counter() - r0) * 1e3
         n_rules = len(ctx.rule_counters())
-        reduce_info = {"rccl_allreduce_u64_words": SHARD_AND_PORT_WORDS + n_rules, "ms": round(group.max(r_ms), 3),
-                       "pkts_reduced": int(red_tot["rx"]), "expected_pkts": world * (args.warmup + args.steps) * B}
-        assert red_tot["rx"] == world * (args.warmup + args.steps) * B, (red_tot, world, args.steps)
+        want = [world * (args.warmup + args.steps) * B] + [world * args.steps * B] * (len(reduce_runs) - 1)
+        res["reduce_info"] = {"rccl_allreduce_u64_words": SHARD_AND_PORT_WORDS + n_rules,
+                              "ms": round(group.max(r_ms), 3), "pkts_reduced_per_interval": reduce_runs,
+                              "expected_per_interval": want, "ok": reduce_runs == want}
+        if reduce_runs != want:
+            log(f"[rank {rank}] RCCL interval sums {reduce_runs} differ from the packets run {want}")
         log(f"[rank {rank}] rccl counter all-reduce of {SHARD_AND_PORT_WORDS + n_rules} u64: {r_ms:.3f} ms")
 
     # ---- kernel duration per launch (HIP events on the context stream) ----
@@ -410,12 +461,148 @@ def main():
     ctx.sync()
     ctx.counters(reset=True)
     ctx.launch_timing(True)
-    nl = max(8, min(200, args.steps // Lb))
+    nl = max(8, min(200, args.steps // Lb)) if primary else 8
     run_steps(0, nl * Lb)
     ctx.sync()
     mean_ms, n_launch = ctx.launch_timing_read(reset=True)
     ctx.launch_timing(False)
     cnt = ctx.counters()
+    res.update(mean_ms=mean_ms, n_launch=n_launch, nl=nl, cnt=cnt)
+    fwd_frac = cnt["forward"] / max(1, cnt["rx"])
+    # algorithmic bytes per packet: the 64 B header line (+4 B offset for
+    # IMIX), the 8 B result record, 4 B per forwarded packet for the
+    # ordered forward list, and its counts (4 B per 256-packet segment, or
+    # per batch)
+    bytes_per_pkt = (76 if W["imix"] else 72) + 4 * fwd_frac + 4.0 * cnt_per_slot / B
+    alg_bytes = bytes_per_pkt * B * Lb
+    achieved = alg_bytes / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
+    res.update(bytes_per_pkt=bytes_per_pkt, alg_bytes=alg_bytes, achieved=achieved, total_pkts=total_pkts)
+    try:   # a report only: never fails the line
+        if W["imix"]:
+            probes = table_probes(fw_tab, rt_tab, slab, offs, args.route_form)
+        else:
+            sample = cg.gen_trace(copdist.shard_seed(0x5EED0000 + cid, rank, 0), B, fw_rules, routes)
+            probes = table_probes(fw_tab, rt_tab, sample, None, args.route_form)
+    except Exception as e:  # noqa: BLE001
+        probes = {"error": repr(e)}
+    res["probes"] = probes
+    ppp, tables = dir_probes_per_pkt(probes) if "error" not in probes else (0.0, 0)
+    if tables:
+        g = probe_ceiling(ctx, tables)
+        if g:
+            kernel_pkt_s = B * Lb / (mean_ms * 1e-3)
+            res["probe"] = {"per_pkt": round(ppp, 4), "tables": tables,
+                            "kernel_gprobes_s": round(ppp * kernel_pkt_s / 1e9, 2),
+                            "ceiling_gprobes_s": round(g, 2),
+                            "probe_bound": round(ppp * kernel_pkt_s / 1e9 / g, 4),
+                            "ceiling_what": f"same box: uniformly random dword loads into {tables} table(s) of "
+                                            f"2^24 u32 (the tbl24 size), 8 packets x {tables} probe(s) per lane in "
+                                            f"flight (tools/probe_kernels.h)"}
+    traffic = None
+    tpath = os.path.join(TRAFFIC_DIR, f"traffic_{name}_L{Lb}_{args.lists}.json")
+    if os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+    res["traffic"] = traffic
+    return res, ctx
+
+
+def roofline_block(res, world, group, args):
+    achieved, alg_bytes = res["achieved"], res["alg_bytes"]
+    ach_min, ach_max, ach_sum = group.min(achieved), group.max(achieved), group.sum(achieved)
+    traffic = res["traffic"]
+    out = {
+        "bound": "hbm",
+        "achieved": round(achieved, 2),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        # the timed region itself: algorithmic bytes of the K timed steps
+        # on all GPUs / the timed elapsed / (peak x GPUs) — launch, ramp,
+        # tail and host sync included (frac is the kernel steady state)
+        "frac_timed": round(res["bytes_per_pkt"] * res["total_pkts"] / res["elapsed"] / 1e9 / (HBM_PEAK_GBS * world),
+                            4),
+        "traffic": traffic,
+        "algorithmic_bytes_per_pkt": round(res["bytes_per_pkt"], 3),
+        "traffic_per_algorithmic": (round(traffic / alg_bytes, 4) if traffic else None),
+        "traffic_source": (f"bench_traffic/traffic_{res['name']}_L{res['Lb']}_{args.lists}.json (rocprofv3 PMC, "
+                           f"tools/pmc_traffic.py)" if traffic else None),
+        "kernel_ms_per_launch": round(res["mean_ms"], 6),
+        "launches_timed": int(res["n_launch"]),
+        "batches_per_launch": res["Lb"],
+        "all_gpus": {"n": world, "achieved_sum": round(ach_sum, 2), "peak_sum": HBM_PEAK_GBS * world,
+                     "frac": round(ach_sum / (HBM_PEAK_GBS * world), 4),
+                     "per_gpu_min": round(ach_min, 2), "per_gpu_max": round(ach_max, 2)},
+        "table_probes": res["probes"],
+    }
+    if "probe" in res:
+        out["probe_bound"] = res["probe"]["probe_bound"]
+        out["probe_ceiling"] = res["probe"]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--allow-shared-gpu", action="store_true",
+                    help="let more ranks than visible GPUs run (they share GPUs; the line says so)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="test the launch and rank protocol only: no GPU, fake timings (CPU tests)")
+    ap.add_argument("--dry-run-devices", type=int, default=8, help="GPUs a --dry-run pretends to see")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help="--dry-run: this rank exits 3 at start")
+    ap.add_argument("--steps", type=int, default=16384)
+    ap.add_argument("--warmup", type=int, default=2048)
+    ap.add_argument("--workload", default="fw1k", choices=sorted(WORKLOADS))
+    ap.add_argument("--secondary", default="auto", choices=("auto", "none", "fw_lpm"),
+                    help="also time this workload in the same run (auto: fw_lpm, the north-star FW + LPM pipeline, "
+                         "when the primary is fw1k)")
+    ap.add_argument("--per-launch", type=int, default=0,
+                    help="batches per kernel launch (ring submit, at most 1024; 0: the workload's default). The "
+                         "~23 us per-launch ramp and tail cost 6 %% at 384 batches, 2.5 %% at 1024")
+    ap.add_argument("--streams", type=int, default=1, help="launch lanes (concurrent streams)")
+    ap.add_argument("--engine", default="auto", choices=("auto", "pmd", "launch"),
+                    help="pmd: the poll-mode kernel serves the batch ring (steps are posted to it); launch: one "
+                         "kernel launch per --per-launch steps; auto: pmd for short runs (< 1024 steps: no "
+                         "per-launch ramp), launch for long runs (large launches stream faster)")
+    ap.add_argument("--pool-mib", type=int, default=0,
+                    help="distinct input bytes per GPU (0: max(400 MiB, one launch of batches))")
+    ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the value is their median")
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-rule-counters", action="store_true", help="ablation: config 5 without per-rule counters")
+    ap.add_argument("--no-rccl-check", action="store_true",
+                    help="skip the untimed RCCL all-reduce of the ranks' counters at the end")
+    ap.add_argument("--stages", type=int, default=0, help="ablation: override the workload's stage mask")
+    ap.add_argument("--no-compact", action="store_true", help="ablation: no ordered forward lists")
+    ap.add_argument("--lists", default="seg", choices=("seg", "dense"),
+                    help="ordered forward lists: seg = 256-packet segments (COP_CFG_SEG_LISTS: per-segment "
+                         "lists + counts, no cross-tile prefix), dense = one list per batch (decoupled look-back)")
+    ap.add_argument("--route-form", default="dir", choices=("dir", "trie"),
+                    help="route tables too large for LDS: DIR-24-8 image (HBM / Infinity Cache) or the multibit "
+                         "trie (12-bit LDS top level + L2-resident 6-bit nodes)")
+    args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    rank, world, local = copdist.env()
+    secondary = args.secondary
+    if secondary == "auto":
+        secondary = "fw_lpm" if args.workload == "fw1k" else "none"
+
+    if args.dry_run:
+        return dry_run(args, rank, world, local, WORKLOADS[args.workload])
+    cg.lib()   # load the HIP runtime the product links (before torch)
+    ndev = cg.device_count()
+    check_devices(args, world, local, ndev)
+    dev = copdist.device_for(local, ndev)
+    group = copdist.Group(rank, world, "gloo")
+
+    res, ctx = measure(args, args.workload, rank, world, dev, group, primary=True)
+    W, B, P, Lb = res["W"], res["B"], res["P"], res["Lb"]
+    ranks_info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(res["own_rate"], 3),
+                                   **({"rccl_init": res["coll"]} if res["rc_on"] else {})})
 
     # ---- single-batch latency: one batch per launch, nothing
     # else in flight; kernel time from HIP events, submit->sync on the host ----
@@ -424,7 +611,7 @@ def main():
     ctx.launch_timing(True)
     for i in range(n_lat):
         h0 = time.perf_counter()
-        ctx.submit_ring(ring, i % P, 1)
+        ctx.submit_ring(res["ring"], i % P, 1)
         ctx.sync()
         host_us.append((time.perf_counter() - h0) * 1e6)
     lat_ms, _ = ctx.launch_timing_read(reset=True)
@@ -436,7 +623,7 @@ def main():
     # every coprocessor, switch.c:33-90), checked against the packets each rank
     # ran since the reset above; untimed, and a failure is reported, not fatal
     allreduce_check = None
-    if not rc_on and not args.no_rccl_check:
+    if not res["rc_on"] and not args.no_rccl_check:
         try:
             ctx.sync()
             uid = group.broadcast_bytes(cg.coll_unique_id() if rank == 0 else None)
@@ -445,48 +632,38 @@ def main():
             r0 = time.perf_counter()
             tot, _ = ctx.coll_reduce_counters(reset=False, with_rules=False)
             r_ms = (time.perf_counter() - r0) * 1e3
-            want = world * (nl * Lb + n_lat) * B
+            want = world * (res["nl"] * Lb + n_lat) * B
             allreduce_check = {"ranks": world, "u64_words": SHARD_AND_PORT_WORDS, "ms": round(group.max(r_ms), 3),
                                "rx_sum": int(tot["rx"]), "rx_expected": want, "ok": int(tot["rx"]) == want}
         except Exception as e:   # noqa: BLE001 (reported in the line)
             allreduce_check = {"ranks": world, "error": str(e)[:200]}
         log(f"[rank {rank}] rccl counter check: {allreduce_check}")
-    fwd_frac = cnt["forward"] / max(1, cnt["rx"])
-    # algorithmic bytes per packet: the 64 B header line (+4 B offset for
-    # IMIX), the 8 B result record, 4 B per forwarded packet for the
-    # ordered forward list, and its counts (4 B per 256-packet segment, or
-    # per batch)
-    bytes_per_pkt = (76 if W["imix"] else 72) + 4 * fwd_frac + 4.0 * cnt_per_slot / B
-    alg_bytes = bytes_per_pkt * B * Lb
-    achieved = alg_bytes / (mean_ms * 1e-3) / 1e9 if mean_ms > 0 else 0.0
 
     # the same box's streaming ceiling for this byte mix (tools/ceiling.hip):
     # read every 64 B slot of the pool, write an 8 B record, nothing else
-    ceiling, ceiling_how = None, None
+    ceiling = None
     if not W["imix"]:
-        ceiling, ceiling_how = box_ceiling(d_pkts.addr, P * B, d_res.addr) or (None, None)
+        ceiling = box_ceiling(res["d_pkts"].addr, P * B, res["d_res"].addr)
 
-    # every GPU's own kernel rate (N > 1: the roofline line is rank 0's
-    # kernel; these give the spread and the node-wide sum against N x peak)
-    ach_min, ach_max, ach_sum = group.min(achieved), group.max(achieved), group.sum(achieved)
-
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_L{Lb}_s{args.streams}.json")
-    if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    roof = roofline_block(res, world, group, args)
+    if ceiling is not None:
+        roof["box_ceiling"] = {
+            "what": "same pool, same process: read each 64 B slot + write an 8 B record, no classification "
+                    "(tools/ceiling.hip: the best of grid-stride copies and per-wave LDS-DMA rings)",
+            "best_pattern": ceiling[1], "achieved": round(ceiling[0], 2), "unit": "GB/s",
+            "frac_of_peak": round(ceiling[0] / HBM_PEAK_GBS, 4),
+            "pipeline_frac_of_ceiling": round(res["achieved"] / ceiling[0], 4),
+            "patterns": ceiling[2]}
 
     out = {
         "metric": METRIC,
-        "value": round(value, 3),
+        "value": round(res["value"], 3),
         "unit": "Mpkt/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed * 1e3 / args.steps, 6),
-        "runs_ms": [round(x * 1e3, 4) for x in runs],
+        "ms_per_step": round(res["elapsed"] * 1e3 / args.steps, 6),
+        "runs_ms": [round(x * 1e3, 4) for x in res["runs"]],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -502,67 +679,52 @@ def main():
             "route_prefixes": W["routes"],
             "route_form": args.route_form if W["routes"] else None,
             "pkt_layout": "imix slab + u32 offsets" if W["imix"] else "64B slots",
-            "stages": W["stages"],
+            "stages": args.stages or W["stages"],
             "parallelism": f"independent per-GPU contexts x{world} (no data-path collective)",
             "pool_batches": int(P),
-            "rule_counters": rc_on,
-            "engine": args.engine,
+            "rule_counters": res["rc_on"],
+            "engine": res["engine"],
             "fwd_lists": ("none (ablation)" if args.no_compact else
                           "segmented: per 256-packet segment an ordered list + count (COP_CFG_SEG_LISTS)"
                           if args.lists == "seg" else "dense: one ordered list per batch (decoupled look-back)"),
             "ranks": ranks_info,
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 2),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            # the timed region itself: algorithmic bytes of the K timed steps
-            # on all GPUs / the timed elapsed / (peak x GPUs) — launch, ramp,
-            # tail and host sync included (frac is the kernel steady state)
-            "frac_timed": round(bytes_per_pkt * total_pkts / elapsed / 1e9 / (HBM_PEAK_GBS * world), 4),
-            "traffic": traffic,
-            "algorithmic_bytes_per_pkt": round(bytes_per_pkt, 3),
-            "traffic_per_algorithmic": (round(traffic / alg_bytes, 4) if traffic else None),
-            "kernel_ms_per_launch": round(mean_ms, 6),
-            "launches_timed": int(n_launch),
-            "all_gpus": {"n": world, "achieved_sum": round(ach_sum, 2), "peak_sum": HBM_PEAK_GBS * world,
-                         "frac": round(ach_sum / (HBM_PEAK_GBS * world), 4),
-                         "per_gpu_min": round(ach_min, 2), "per_gpu_max": round(ach_max, 2)},
-            "box_ceiling": (None if ceiling is None else {
-                "what": "same pool, same process: read each 64 B slot + write an 8 B record, no classification "
-                        "(tools/ceiling.hip: best of a grid-stride copy and per-wave LDS-DMA rings)",
-                "best_pattern": ceiling_how,
-                "achieved": round(ceiling, 2), "unit": "GB/s",
-                "frac_of_peak": round(ceiling / HBM_PEAK_GBS, 4),
-                "pipeline_frac_of_ceiling": round(achieved / ceiling, 4)}),
-        },
+        "roofline": roof,
         "cpu_baseline": None,
     }
     out["single_batch_latency"] = single_batch
-    try:   # a report only: never fails the line
-        if W["imix"]:
-            probes = table_probes(fw_tab, rt_tab, slab, offs, args.route_form)
-        else:
-            sample = cg.gen_trace(copdist.shard_seed(0x5EED0000 + cid, rank, 0), B, fw_rules, routes)
-            probes = table_probes(fw_tab, rt_tab, sample, None, args.route_form)
-        out["roofline"]["table_probes"] = probes
-    except Exception as e:  # noqa: BLE001
-        out["roofline"]["table_probes"] = {"error": repr(e)}
-    if pmd_info:
+    if "pmd_info" in res:
         # the poll-mode kernel: a 1024-batch post (HBM-resident, one post, no
         # launch) timed on the host, as a fraction of the peak
-        pmd_info["steady_frac"] = round(pmd_info["steady_mpkt_s"] * 1e6 * bytes_per_pkt / 1e9 / HBM_PEAK_GBS, 4)
-        out["pmd"] = pmd_info
-    if reduce_info:
-        out["counter_reduce"] = reduce_info
+        pi = res["pmd_info"]
+        pi["steady_frac"] = round(pi["steady_mpkt_s"] * 1e6 * res["bytes_per_pkt"] / 1e9 / HBM_PEAK_GBS, 4)
+        out["pmd"] = pi
+    if "reduce_info" in res:
+        out["counter_reduce"] = res["reduce_info"]
     if allreduce_check:
         out["counter_allreduce_check"] = allreduce_check
+    ctx.close()
+
+    # ---- the north-star workload (FW + LPM 100k, 64 B) in the same run ----
+    if secondary != "none":
+        try:
+            sres, sctx = measure(args, secondary, rank, world, dev, group, primary=False)
+            sroof = roofline_block(sres, world, group, args)
+            out["secondary"] = {secondary: {
+                "description": sres["W"]["desc"], "value": round(sres["value"], 3), "unit": "Mpkt/s",
+                "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": round(sres["elapsed"] * 1e3 / args.steps, 6),
+                "runs_ms": [round(x * 1e3, 4) for x in sres["runs"]], "engine": sres["engine"],
+                "route_form": args.route_form, "roofline": sroof}}
+            sctx.close()
+        except Exception as e:  # noqa: BLE001 (the primary line stands)
+            out["secondary"] = {secondary: {"error": str(e)[:300]}}
+            log(f"[rank {rank}] secondary {secondary} failed: {e}")
 
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as orc   # CPU baseline leg only
+        fw_rules = res["fw_rules"]
         ofw = orc.OracleLpm(max(1024, W["fw"]), 24 if W["fw"] <= 1000 else 1 << 20)
         ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=W["fw"] <= 1000)
         ns = 131072
@@ -571,23 +733,31 @@ def main():
         # process's main thread and the driver's interrupts)
         core = max(os.sched_getaffinity(0))
         rate, pk, secs = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget, 1, core)
+        model = cpu_model()
         out["cpu_baseline"] = {
             "value": round(rate, 3),
             "unit": "Mpkt/s",
             "cores": 1,
             "kind": "port",
+            "cpu_model": model,
             "sample": (f"{pk} packets through the restated coprocessor() loop (burst 32, 16384-slot "
                        f"SPSC ring, 2176 B mbufs, DIR-24-8 firewall, {W['fw']} rules), "
-                       f"{secs:.1f} s on 1 pinned core (cpu {core})"),
+                       f"{secs:.1f} s on 1 pinned core (cpu {core}, {model})"),
         }
         log(f"[rank 0] cpu baseline {rate:.1f} Mpkt/s on 1 core ({pk} pkts)")
-        # one coprocessor thread per host core this job may
-        # use (the box's CPU share: OMP_NUM_THREADS, affinity), unpinned
-        ncores = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "8")), 32))
+        # one coprocessor thread per host core of this
+        # job's CPU share. The affinity mask of a GPU box lists every core of
+        # the host, but the job's share is $OMP_NUM_THREADS (16 on the pool's
+        # one-GPU boxes): the leg uses that many, and says so
+        affinity = len(os.sched_getaffinity(0))
+        share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+        ncores = max(1, min(affinity, share if share > 0 else affinity))
         if ncores > 1:
             rate_m, pk_m, secs_m = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget / 2, ncores, -1)
             out["cpu_baseline_multicore"] = {
-                "value": round(rate_m, 3), "unit": "Mpkt/s", "cores": ncores, "kind": "port",
+                "value": round(rate_m, 3), "unit": "Mpkt/s", "cores": ncores, "kind": "port", "cpu_model": model,
+                "cores_note": (f"the job's CPU share: OMP_NUM_THREADS={share} of {affinity} cores in the affinity "
+                               f"mask" if share > 0 else f"every core of the affinity mask ({affinity})"),
                 "sample": (f"{pk_m} packets, {ncores} threads each running the restated coprocessor() loop "
                            f"on its own rings and mbuf pool, {secs_m:.1f} s"),
             }
@@ -595,31 +765,51 @@ def main():
 
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
     group.close()
 
 
 def dry_run(args, rank, world, local, W):
     """The launch/rank protocol with the GPU leg stubbed: device checks,
-    gloo rendezvous, barrier-bracketed fake timings, max over ranks, the
-    per-rank gather and rank 0's one JSON line (CPU tests of --gpus N)."""
+    gloo rendezvous, the RCCL unique-id broadcast and the counter reduction
+    of rule-counter workloads (gloo sum standing in for the all-reduce, its
+    mismatch reported, not asserted), barrier-bracketed fake timings, max
+    over ranks, the per-rank gather and rank 0's one JSON line (CPU tests of
+    --gpus N)."""
+    if rank == args.dry_run_fail_rank:
+        log(f"[rank {rank}] dry-run: failing on purpose")
+        sys.exit(3)
     check_devices(args, world, local, args.dry_run_devices)
     dev = copdist.device_for(local, args.dry_run_devices)
     group = copdist.Group(rank, world, "gloo")
     B = W["batch"]
-    runs, own = [], []
+    rc_on = bool(W.get("rule_counters")) and not args.no_rule_counters
+    coll, reduce_info = None, None
+    if rc_on:
+        uid = group.broadcast_bytes(bytes(range(128)) if rank == 0 else None)
+        coll = "ok" if uid == bytes(range(128)) else "error: unique id differs"
+    runs, own, reduced = [], [], []
     for r in range(max(1, args.repeats)):
         group.barrier()
         t = 1e-3 * (1.0 + 0.1 * rank)   # rank r "takes" (1 + r/10) ms per run
+        if rc_on:
+            pk = (args.warmup if r == 0 else 0) + args.steps
+            reduced.append(int(group.sum_u64(np.array([pk * B], np.uint64))[0]))
         own.append(t)
         group.barrier()
         runs.append(group.max(t))
+    if rc_on:
+        want = [world * (args.warmup + args.steps) * B] + [world * args.steps * B] * (len(reduced) - 1)
+        reduce_info = {"pkts_reduced_per_interval": reduced, "expected_per_interval": want, "ok": reduced == want}
     elapsed = float(np.median(runs))
-    info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(args.steps * B / float(np.median(own)) / 1e6, 3)})
+    info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(args.steps * B / float(np.median(own)) / 1e6, 3),
+                             **({"rccl_init": coll} if rc_on else {})})
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": round(world * args.steps * B / elapsed / 1e6, 3), "unit": "Mpkt/s",
-                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
-                          "config": {"workload": args.workload, "ranks": info}}), flush=True)
+        line = {"metric": METRIC, "value": round(world * args.steps * B / elapsed / 1e6, 3), "unit": "Mpkt/s",
+                "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                "config": {"workload": args.workload, "ranks": info}}
+        if reduce_info:
+            line["counter_reduce"] = reduce_info
+        print(json.dumps(line), flush=True)
     group.close()
 
 

@@ -669,6 +669,10 @@ def make_ring(pkts, n_slots: int, n: int, results, pkts_slot_bytes: int, results
     r.results_slot = results_slot or n
     r.fwd_slot = fwd_slot or n
     r.n_slots, r.n, r.stride, r.data_off = n_slots, n, stride, data_off
+    # the ring holds device addresses only: keep the buffers it was made from
+    # alive as long as the ring (a collected DeviceBuffer frees its memory,
+    # and a kernel writing through the stale address would fault the GPU)
+    r._keep = tuple(x for x in (pkts, offsets, results, fwd_idx, fwd_count) if isinstance(x, DeviceBuffer))
     return r
 
 
@@ -688,4 +692,5 @@ def make_batch(pkts: DeviceBuffer | int, n: int, results: DeviceBuffer | int, st
     b.results = addr(results, results_offset)
     b.fwd_idx = addr(fwd_idx)
     b.fwd_count = addr(fwd_count)
+    b._keep = tuple(x for x in (pkts, offsets, results, fwd_idx, fwd_count) if isinstance(x, DeviceBuffer))
     return b

@@ -923,6 +923,114 @@ __device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, co
     }
 }
 
+// The tile's verdict counters as wave-uniform totals from ballots (scalar
+// popcounts: no cross-lane reduction chains). Same values as the per-lane
+// Counts of pass2 + store_records summed over the wave.
+template <int FW, int PPT>
+__device__ __forceinline__ Counts wave_counts(const bool (&valid)[PPT], const uint32_t (&verdict)[PPT],
+                                              const uint32_t (&flags)[PPT])
+{
+    Counts c;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        const uint32_t v = verdict[k];
+        const bool in = valid[k];
+        const bool reached = v != COPK_DROP_PARSE && v != COPK_DROP_NO_PORT;
+        c.rx += (uint32_t)__popcll(__ballot(in));
+        c.fwd += (uint32_t)__popcll(__ballot(in && v == COPK_FORWARD));
+        c.dropfw += (uint32_t)__popcll(__ballot(in && v == COPK_DROP_FW));
+        c.parse += (uint32_t)__popcll(__ballot(in && v == COPK_DROP_PARSE));
+        c.noport += (uint32_t)__popcll(__ballot(in && v == COPK_DROP_NO_PORT));
+        c.rhit += (uint32_t)__popcll(__ballot(in && (flags[k] & COPK_FLAG_ROUTE_HIT)));
+        if (FW != COPK_TBL_OFF) {
+            c.total += (uint32_t)__popcll(__ballot(in && reached));
+            c.notv4 += (uint32_t)__popcll(__ballot(in && v == COPK_DROP_NOT_IPV4));
+        }
+    }
+    return c;
+}
+
+// The counters' per-workgroup adds (after a barrier that follows every
+// wave's s_red writes): cop_counters order, one atomic per counter.
+__device__ __forceinline__ void counters_add(const CopKParams &p, const uint32_t *s_red, int tid)
+{
+    if (tid < 9) {
+        uint32_t r[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int w = 0; w < WAVES; w++) v += s_red[w * 8 + q];
+            r[q] = v;
+        }
+        // s_red order: total, notv4, fwd, dropfw, parse, noport, rhit, rx;
+        // cop_counters order: drop, accept, not_ipv4, total, parse_err, no_port, forward, route_hit, rx
+        const uint32_t v = tid == 0 ? r[3] + r[1] : tid == 1 ? r[0] - r[1] - r[3] : tid == 2 ? r[1] : tid == 3 ? r[0]
+                         : tid == 4 ? r[4] : tid == 5 ? r[5] : tid == 6 ? r[2] : tid == 7 ? r[6] : r[7];
+        if (v) atomicAdd(&p.counters[(blockIdx.x % COPK_COUNTER_SHARDS) * 16 + tid], (unsigned long long)v);
+    }
+}
+
+// The segmented-list tile epilogue with the counters folded in (no optional
+// features: COP_CFG_SEG_LISTS without per-rule bins or port statistics).
+// Per (step, wave): ballot of FORWARD; the wave's verdict counters from
+// ballots; one barrier; then each wave stages its packets' list entries at
+// their segment positions, wave 0 writes the segment lengths, the records go
+// out (mid) and nine lanes add the counters; a second barrier; the segments'
+// 16-byte list stores. Two barriers per tile against four for the general
+// path (compaction, counter reduction), and no shuffle reductions.
+template <int FW, int PPT, bool WT, typename Mid>
+__device__ __forceinline__ void seg_epilogue(const CopKParams &p, const CopKBatch &B, uint32_t base,
+                                             const bool (&valid)[PPT], const uint32_t (&verdict)[PPT],
+                                             const uint32_t (&flags)[PPT], const CompactLds &s, uint32_t *s_red,
+                                             int tid, int lane, int wave, Mid mid)
+{
+    static_assert(COPK_SEG == BLOCK, "one segment per tile step");
+    const Counts cw = wave_counts<FW, PPT>(valid, verdict, flags);
+    unsigned long long bal[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) bal[k] = __ballot(valid[k] && verdict[k] == COPK_FORWARD);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < PPT; k++) s.cnt[k * WAVES + wave] = (uint32_t)__popcll(bal[k]);
+        const uint32_t c8[8] = {cw.total, cw.notv4, cw.fwd, cw.dropfw, cw.parse, cw.noport, cw.rhit, cw.rx};
+#pragma unroll
+        for (int q = 0; q < 8; q++) s_red[wave * 8 + q] = c8[q];
+    }
+    lds_barrier();
+    if (B.fwd_idx) {
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            uint32_t off = 0;
+#pragma unroll
+            for (int w = 0; w < WAVES; w++) off += w < wave ? s.cnt[k * WAVES + w] : 0u;
+            if ((bal[k] >> lane) & 1ull)
+                s.stage[k * BLOCK + off +
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[k] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[k], 0u))] =
+                    base + k * BLOCK + tid;
+        }
+    }
+    if (B.fwd_count && wave == 0 && lane < PPT && base + (uint32_t)lane * BLOCK < B.n) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; w++) c += s.cnt[lane * WAVES + w];
+        st_u32<WT>(c, B.fwd_count + base / COPK_SEG + (uint32_t)lane);
+    }
+    mid();
+    counters_add(p, s_red, tid);
+    lds_barrier();
+    if (B.fwd_idx) {
+        for (uint32_t q = (uint32_t)tid; q < (uint32_t)PPT * (BLOCK / 4); q += BLOCK) {
+            const uint32_t k = q / (BLOCK / 4), cc = q % (BLOCK / 4);
+            uint32_t c = 0;
+#pragma unroll
+            for (int w = 0; w < WAVES; w++) c += s.cnt[k * WAVES + w];
+            if (cc * 4u < c)
+                st_u32x4<WT>(*(const u32x4 *)&s.stage[k * BLOCK + cc * 4u], B.fwd_idx, (long)(base + k * BLOCK + cc * 4u));
+        }
+    }
+}
+
 // Per-port coprocessor_stats (switch.h:33-38) of one tile, added to
 // wave-uniform accumulators: rx = packets routed to the port's NF
 // (enqueue_nf_rx), tx = packets it forwarded.

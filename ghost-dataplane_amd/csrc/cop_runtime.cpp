@@ -2027,10 +2027,12 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         p.dbg = 0;   // no ablations in the persistent kernel
         p.stamps = nullptr;
         const char *stamps_env = getenv("COP_PMD_STAMPS");
-        if (stamps_env && atoi(stamps_env) >= 2) {   // diagnostic: the tile body's phase stamps too (EXT kernel)
+        if (stamps_env && atoi(stamps_env) >= 2) {   // diagnostic: the tile body's phase stamps too
             if (hipMalloc(&p.stamps, (size_t)c->ncu * 8 * 8 * 8) != hipSuccess)
                 PMD_FAIL(set_err(c, -ENOMEM, "pmd: stamps"));
-            p.dbg = 8;
+            // 2: through the EXT kernel (dbg bit 8); 3: the production kernel
+            // of a -DCOPK_PHASE_STAMPS=1 experiment build
+            if (atoi(stamps_env) == 2) p.dbg = 8;
         }
         // per-rule hits by binning, as in the one-shot kernel: one region per
         // (slot, tile), counted by cop_hit_count beside the running kernel

@@ -8,10 +8,16 @@
 namespace copd {
 
 // diagnostic-only phase stamps (p.dbg bit 8): wave 0 lane 0 writes
-// s_memrealtime (100 MHz) per phase into a buffer nothing else reads
+// s_memrealtime (100 MHz) per phase into a buffer nothing else reads.
+// Experiment builds with -DCOPK_PHASE_STAMPS=1 stamp whenever p.stamps is
+// set, so the production (non-EXT) kernels can be stamped at their own
+// occupancy.
+#ifndef COPK_PHASE_STAMPS
+#define COPK_PHASE_STAMPS 0
+#endif
 #define STAMP(ph)                                                                          \
     do {                                                                                   \
-        if ((o.dbg & 8u) && tid == 0) {                                                    \
+        if (((o.dbg & 8u) || (COPK_PHASE_STAMPS && p.stamps)) && tid == 0) {               \
             __builtin_amdgcn_sched_barrier(0);                                             \
             __hip_atomic_store(&p.stamps[blockIdx.x * 8 + (ph)], __builtin_amdgcn_s_memrealtime(), \
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                     \
@@ -273,6 +279,22 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
     Counts cn;
     pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, cn.total, cn.notv4);
     const bool bins = EXT && FW != COPK_TBL_OFF && p.hit_region != nullptr;
+    // segmented lists with no optional feature: the lean epilogue (counters
+    // from ballots, folded into the list's barriers)
+    if (!EXT && p.seg && p.compact && !(o.dbg & 64u)) {
+        STAMP(3);
+        const bool paired = p.rec_paired != 0;
+        bool fwd[PPT];
+        Counts dummy;
+        auto records = [&] {
+            if (paired) store_records_paired<PPT, WT>(B, base, tid, lane, wave, valid, verdict, flags, port, rnh, fwd, dummy);
+            else store_records<PPT, WT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, dummy, nullptr);
+        };
+        seg_epilogue<FW, PPT, WT>(p, B, base, valid, verdict, flags, lc.cl, lc.s_red, tid, lane, wave, records);
+        STAMP(5);
+        STAMP(6);
+        return;
+    }
     if (bins) hit_hist<PPT>(hit_lds<PPT>(p, lc.s_misc - p.lds_misc_off), valid, flags, fwe, tid, p.hit_nb == 1);
     else rule_hit_atomics<FW, PPT>(o, valid, flags, fwe);
     if (o.dbg & 8u) {

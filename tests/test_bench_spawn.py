@@ -59,3 +59,32 @@ def test_world_size_must_match_gpus():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run"], capture_output=True, text=True,
                        timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_two_ranks_rule_counter_workload_protocol():
+    """The config-5 branches the 8-GPU run takes: the RCCL unique-id
+    broadcast from rank 0, the per-interval counter reduction (gloo standing
+    in for the RCCL all-reduce) checked and reported — not asserted — and
+    each rank's RCCL init status in config.ranks."""
+    r = run("--gpus", "2", "--dry-run", "--workload", "fw_lpm_1m", "--steps", "20", "--warmup", "5", "--repeats", "3")
+    assert r.returncode == 0, r.stderr
+    lines = json_lines(r.stdout)
+    assert len(lines) == 1
+    line = lines[0]
+    assert [x["rccl_init"] for x in line["config"]["ranks"]] == ["ok", "ok"]
+    red = line["counter_reduce"]
+    B = 262144
+    assert red["ok"] and red["pkts_reduced_per_interval"] == [2 * 25 * B, 2 * 20 * B, 2 * 20 * B]
+
+
+def test_failing_rank_ends_the_others_fast():
+    """One rank exits at start (as a table or device error would): the parent
+    ends the rank left waiting in the gloo rendezvous and returns the failure
+    at once, not after gloo's long timeout."""
+    import time as _t
+    t0 = _t.time()
+    r = run("--gpus", "2", "--dry-run", "--dry-run-fail-rank", "1", "--steps", "4", "--warmup", "0", "--repeats", "1",
+            timeout=120)
+    assert r.returncode != 0
+    assert _t.time() - t0 < 60
+    assert "failed first" in r.stderr

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--posts", default="1,20,64,128")
     ap.add_argument("--lists", default="seg", choices=("seg", "dense"))
+    ap.add_argument("--dump", default="", help="save each post's raw stamps to <prefix>_post<k>.npz")
     args = ap.parse_args()
     fw = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
     B, P = 65536, 128
@@ -77,6 +78,11 @@ def main():
                   "compaction+records": tb[:, 5] - tb[:, 3], "counters": tb[:, 6] - tb[:, 5]}
             print("   body phases (median/max us): " + "; ".join(f"{k2} {us(np.median(v)):.2f}/{us(v.max()):.2f}"
                                                               for k2, v in ph.items()))
+        if args.dump:
+            # raw stamps of this post's tiles (worker = row index), for offline analysis
+            sel = np.isin(st[:, 4], list(last_batches))
+            extra = buf[G * 8 + 128:G * 16 + 128].reshape(G, 8).astype(np.int64) if n > G * 8 + 128 else None
+            np.savez(f"{args.dump}_post{k}.npz", stamps=st, sel=sel, relay=t_relay, phases=extra)
         # when the tiles of the post finished, relative to the relay (us): quantiles
         q = np.percentile(end, [10, 50, 90, 99, 100])
         sq = np.percentile(seen, [10, 50, 90, 100])

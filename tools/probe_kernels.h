@@ -64,6 +64,19 @@ __global__ __launch_bounds__(256) void probe_pair(const uint32_t *__restrict__ t
     out[gid] = x ^ y;
 }
 
+// Both loads of the pair issued back to back (plain loads, as the
+// pipeline's probes), then used: a second load into the same line while the
+// first miss is outstanding merges with it if the fill covers both offsets.
+__global__ __launch_bounds__(256) void probe_pair_sim(const uint32_t *__restrict__ t, uint32_t lines, uint32_t a,
+                                                      uint32_t b, uint64_t seed, uint32_t *__restrict__ out)
+{
+    const uint64_t gid = blockIdx.x * 256ull + threadIdx.x;
+    const uint32_t line = (uint32_t)mix64(seed ^ gid) & (lines - 1);
+    const uint32_t *p = t + (size_t)line * 32;
+    const uint32_t x = p[a / 4], y = p[b / 4];
+    out[gid] = x ^ y;
+}
+
 }  // namespace probek
 
 #endif

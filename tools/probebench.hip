@@ -12,6 +12,9 @@
 //   pair64   : per lane one probe, then an L1-bypassing load 64 B further in
 //              the same 128-byte line (fill granularity: 1 or 2 requests)
 //   pair32   : the same 32 B further (same 64-byte half: always 1 request)
+//   spair64/32: the two loads issued together (plain loads: a miss fill that
+//              covers both offsets merges them into one request)
+//   rand16g  : a 16 GiB table (almost no Infinity-Cache hits)
 // Prints one line per case: name, probes, median us, Gprobes/s.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -80,5 +83,26 @@ int main()
     timeit("pair32", lanes * 2, [&](uint64_t s) {
         hipLaunchKernelGGL(probek::probe_pair, dim3(grid), dim3(256), 0, 0, tb, (uint32_t)(big / 128), 0u, 32u, s, out);
     });
+    timeit("spair64", lanes * 2, [&](uint64_t s) {
+        hipLaunchKernelGGL(probek::probe_pair_sim, dim3(grid), dim3(256), 0, 0, tb, (uint32_t)(big / 128), 0u, 64u, s,
+                           out);
+    });
+    timeit("spair32", lanes * 2, [&](uint64_t s) {
+        hipLaunchKernelGGL(probek::probe_pair_sim, dim3(grid), dim3(256), 0, 0, tb, (uint32_t)(big / 128), 0u, 32u, s,
+                           out);
+    });
+    // a 16 GiB table: Infinity-Cache hits ~1.6 %, so the rate is what HBM
+    // serves for isolated probes (128-byte fills would cap it near 6.3 TB/s /
+    // 128 B = 49 Gprobes/s)
+    uint32_t *th = nullptr;
+    const size_t huge = (size_t)16 << 30;
+    if (hipMalloc(&th, huge) == hipSuccess) {
+        CHK(hipMemset(th, 0x44, huge));
+        timeit("rand16g", lanes * 8 * rounds, [&](uint64_t s) {
+            hipLaunchKernelGGL(probek::probe_rand<8>, dim3(grid), dim3(256), 0, 0, th, th, (uint32_t)(huge / 4 - 1) + 1u,
+                               1, rounds, s, out);
+        });
+        CHK(hipFree(th));
+    }
     return 0;
 }
