@@ -168,6 +168,9 @@ SIGNATURES = {
     "cop_set_mbuf_layout": (None, [c_uint32, c_uint32]),
     "cop_set_rule_file": (None, [c_char_p]),
     "coprocessor_setup": (c_int, []),
+    "cop_set_dropin_stages": (c_int, [c_uint32]),
+    "cop_dropin_stages": (c_uint32, []),
+    "cop_coprocessor_setup_stages": (c_int, [c_uint32]),
     "coprocessor_teardown": (c_int, []),
     "process_packet": (c_int, [c_void_p]),
     "process_burst": (c_int, [c_void_p, c_uint32, c_void_p]),

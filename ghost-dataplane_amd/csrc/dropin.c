@@ -6,10 +6,13 @@
  *   process_packet       coprocessor.c:50-65  (0 forward / -1 drop)
  *   cop_coprocessor_poll switch.c:443-474     (coprocessor() loop body)
  *
- * All of them run COP_DROPIN_STAGES, the NF chain of process_packet
- * (fw_packet_handler, coprocessor.c:59-62): get_next_hop's parse/route
- * drop belongs to the fast path (switch.c:406-415), which has already
- * routed every packet it enqueues to a coprocessor ring.
+ * All of them run the drop-in stage mask, the NF chain of process_packet:
+ * the firewall (fw_packet_handler under ENABLE_FW_NF, coprocessor.c:59-62),
+ * or nothing (coprocessor.c:59-64 without it: every packet forwards);
+ * cop_set_dropin_stages / the COP_DROPIN_STAGES macro of the caller's build
+ * choose. get_next_hop's parse/route drop belongs to the fast path
+ * (switch.c:406-415), which has already routed every packet it enqueues to
+ * a coprocessor ring.
  *
  * The reference calls setup/teardown once per coprocessor lcore, five
  * threads at once (main.c:92-94, switch.c:525,537), with NF state in
@@ -22,12 +25,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#define COP_NO_DROPIN_MACROS 1   /* this file defines the functions the macros call */
 #include "cop_gpu.h"
 #include "cop_internal.h"
 
 static uint32_t g_buf_addr_off = 0;   /* rte_mbuf.buf_addr (DPDK 17.11-19.05) */
 static uint32_t g_data_off_off = 16;  /* rte_mbuf.data_off */
 static char g_rule_file[4096] = "./nfs/firewall/rules.json"; /* coprocessor.c:19 */
+static volatile uint32_t g_dropin_stages = COP_STAGE_FW;       /* ENABLE_FW_NF, coprocessor.h:21 */
 static int g_rule_file_set = 0;
 
 static __thread cop_ctx *tl_ctx = NULL;
@@ -74,6 +79,25 @@ static inline const void *mbuf_data(const struct rte_mbuf *m)
     return (const uint8_t *)addr + off;   /* rte_pktmbuf_mtod */
 }
 
+int cop_set_dropin_stages(uint32_t stages)
+{
+    if (stages & ~COP_STAGE_FW) return -EINVAL;   /* process_packet's chain: the firewall or nothing */
+    g_dropin_stages = stages;
+    return 0;
+}
+
+uint32_t cop_dropin_stages(void)
+{
+    return g_dropin_stages;
+}
+
+int cop_coprocessor_setup_stages(uint32_t stages)
+{
+    int rc = cop_set_dropin_stages(stages);
+    if (rc) return 1;
+    return coprocessor_setup();
+}
+
 cop_ctx *coprocessor_ctx(void)
 {
     return tl_ctx;
@@ -84,7 +108,7 @@ int coprocessor_setup(void)
     if (tl_ctx) return 0;
     cop_config cfg;
     cop_config_default(&cfg);
-    cfg.stages = COP_DROPIN_STAGES;
+    cfg.stages = g_dropin_stages;
     const char *dev = getenv("COP_DEVICE");
     if (dev) cfg.device = atoi(dev);
     int rc = cop_create(&cfg, &tl_ctx);
@@ -178,7 +202,7 @@ int process_burst(struct rte_mbuf **pkts, uint32_t n, int *ret)
     if (!tl_ctx || (n && (!pkts || !ret))) return -EINVAL;
     if (ensure_buf(n)) return -ENOMEM;
     for (uint32_t i = 0; i < n; i++) tl_buf.data[i] = mbuf_data(pkts[i]);
-    int rc = cop_process_host_stages(tl_ctx, COP_DROPIN_STAGES, tl_buf.data, n, tl_buf.res, NULL, NULL);
+    int rc = cop_process_host_stages(tl_ctx, g_dropin_stages, tl_buf.data, n, tl_buf.res, NULL, NULL);
     if (rc) return rc;
     for (uint32_t i = 0; i < n; i++) ret[i] = tl_buf.res[i].verdict == COP_FORWARD ? 0 : -1;
     return 0;
@@ -255,7 +279,7 @@ int cop_coprocessor_poll(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_
     if (ensure_buf(max_pkts)) return -ENOMEM;
     const uint32_t n = drain_rx(rx, tl_buf.objs, tl_buf.data, max_pkts);
     if (n == 0) return 0;
-    int rc = cop_process_host_stages(ctx, COP_DROPIN_STAGES, tl_buf.data, n, tl_buf.res, NULL, NULL);
+    int rc = cop_process_host_stages(ctx, g_dropin_stages, tl_buf.data, n, tl_buf.res, NULL, NULL);
     if (rc) {
         drop_all(tl_buf.objs, n, free_fn, free_arg, stats);
         return rc;
@@ -318,7 +342,7 @@ int cop_coprocessor_poll_async(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_
     }
     const uint32_t n = drain_rx(rx, tl_async.objs[s], tl_async.data, max_pkts);
     if (n) {
-        int rc = cop_host_batch_submit_stages(ctx, COP_DROPIN_STAGES, s, tl_async.data, n);
+        int rc = cop_host_batch_submit_stages(ctx, g_dropin_stages, s, tl_async.data, n);
         if (rc) {
             drop_all(tl_async.objs[s], n, free_fn, free_arg, stats);
             return rc;

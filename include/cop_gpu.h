@@ -58,15 +58,28 @@ extern "C" {
 #endif
 
 /* Stages of the drop-in coprocessor API (process_packet, process_burst,
- * cop_coprocessor_poll*): the coprocessor thread's NF chain only —
- * process_packet runs fw_packet_handler under ENABLE_FW_NF
- * (coprocessor.c:59-62), which coprocessor.h:21 always defines. Parse and
+ * cop_coprocessor_poll*): the coprocessor thread's NF chain only. Parse and
  * vport routing (get_next_hop, the UNKNOWN_PORT drop) are the fast path's
- * job before a packet is enqueued to the coprocessor (switch.c:406-415),
- * so the drop-in never drops on them: an IPv4 packet whose dst&0xFFFF is in
+ * job before a packet is enqueued to the coprocessor (switch.c:406-415), so
+ * the drop-in never drops on them: an IPv4 packet whose dst&0xFFFF is in
  * 0..4, or an IPv6 EtherType, gets the firewall's verdict. The batch API
- * (cop_submit*, cop_process_host*) runs cop_config.stages. */
+ * (cop_submit*, cop_process_host*) runs cop_config.stages.
+ *   - process_packet runs fw_packet_handler under ENABLE_FW_NF
+ *     (coprocessor.c:59-62), which the reference's coprocessor.h:21 always
+ *     defines: COP_STAGE_FW, also when neither macro is defined.
+ *   - DISABLE_NF (coprocessor.h:19): switch.c never calls the coprocessor
+ *     (switch.c:411,426,524); if it is called anyway, every packet forwards
+ *     (no NF stage), as process_packet does without ENABLE_FW_NF
+ *     (coprocessor.c:59-64). Define COP_DROPIN_NO_NF for that chain alone.
+ * The library is built once, so the caller's macros reach it through
+ * coprocessor_setup(), which this header turns into
+ * cop_coprocessor_setup_stages(COP_DROPIN_STAGES) in the caller's build
+ * (cop_set_dropin_stages sets the same at run time, e.g. from an FFI). */
+#if defined(DISABLE_NF) || defined(COP_DROPIN_NO_NF)
+#define COP_DROPIN_STAGES 0u
+#else
 #define COP_DROPIN_STAGES (COP_STAGE_FW)
+#endif
 
 /* Per-packet verdicts (one byte of the result record).
  *   FORWARD/DROP_FW : enum FW_ACTION firewall.h:71-74 (FW_FORWARD=0, FW_DROP=1)
@@ -522,8 +535,19 @@ void cop_set_mbuf_layout(uint32_t buf_addr_off, uint32_t data_off_off);
 void cop_set_rule_file(const char *path);
 
 /* Per calling thread: create a GPU context (device = $COP_DEVICE or 0),
- * load the rule file with the reference limits. 0 or non-zero. */
+ * load the rule file with the reference limits. 0 or non-zero. Runs the
+ * drop-in stage mask (cop_dropin_stages(), COP_STAGE_FW unless set). */
 int coprocessor_setup(void);
+/* The drop-in NF chain for contexts set up afterwards and for the drop-in
+ * calls: COP_STAGE_FW or 0 (no NF: every packet forwards). 0 or -EINVAL. */
+int cop_set_dropin_stages(uint32_t stages);
+uint32_t cop_dropin_stages(void);
+/* cop_set_dropin_stages(stages), then coprocessor_setup(). */
+int cop_coprocessor_setup_stages(uint32_t stages);
+#ifndef COP_NO_DROPIN_MACROS
+/* the caller's ENABLE_FW_NF / DISABLE_NF select the chain (see COP_DROPIN_STAGES) */
+#define coprocessor_setup() cop_coprocessor_setup_stages(COP_DROPIN_STAGES)
+#endif
 int coprocessor_teardown(void);
 /* 0 = forward, -1 = drop (coprocessor.c:50-65). One-packet GPU batch:
  * correct but latency-bound; use process_burst / cop_coprocessor_poll. */
