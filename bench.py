@@ -403,7 +403,7 @@ def measure(args, name, rank, world, dev, group, primary):
         res["slab"], res["offs"] = slab, offs
 
     # ---- the poll-mode kernel's steady state and single-batch latency ----
-    if engine == "pmd" and primary:
+    if engine == "pmd" and primary and not args.quick:
         pmd_on()
         n_long = min(P, 1024)
         longs = []
@@ -487,7 +487,7 @@ def measure(args, name, rank, world, dev, group, primary):
         probes = {"error": repr(e)}
     res["probes"] = probes
     ppp, tables = dir_probes_per_pkt(probes) if "error" not in probes else (0.0, 0)
-    if tables:
+    if tables and not args.quick:
         g = probe_ceiling(ctx, tables)
         if g:
             kernel_pkt_s = B * Lb / (mean_ms * 1e-3)
@@ -496,7 +496,7 @@ def measure(args, name, rank, world, dev, group, primary):
                             "ceiling_gprobes_s": round(g, 2),
                             "probe_bound": round(ppp * kernel_pkt_s / 1e9 / g, 4),
                             "ceiling_what": f"same box: uniformly random dword loads into {tables} table(s) of "
-                                            f"2^24 u32 (the tbl24 size), 8 packets x {tables} probe(s) per lane in "
+                                            f"2^24 u32 (the tbl24 size), 8 or 16 packets x {tables} probe(s) per lane, 8 or 16 workgroups per CU, the best of the four shapes, in "
                                             f"flight (tools/probe_kernels.h)"}
     traffic = None
     tpath = os.path.join(TRAFFIC_DIR, f"traffic_{name}_L{Lb}_{args.lists}.json")
@@ -571,6 +571,9 @@ def main():
     ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the value is their median")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--quick", action="store_true",
+                    help="A/B runs: the timed steps and the kernel roofline only (no poll-mode extras, single-batch "
+                         "latency, ceilings, RCCL check, secondary workload or CPU baseline)")
     ap.add_argument("--no-rule-counters", action="store_true", help="ablation: config 5 without per-rule counters")
     ap.add_argument("--no-rccl-check", action="store_true",
                     help="skip the untimed RCCL all-reduce of the ranks' counters at the end")
@@ -589,7 +592,9 @@ def main():
     rank, world, local = copdist.env()
     secondary = args.secondary
     if secondary == "auto":
-        secondary = "fw_lpm" if args.workload == "fw1k" else "none"
+        secondary = "fw_lpm" if args.workload == "fw1k" and not args.quick else "none"
+    if args.quick:
+        args.no_cpu = args.no_rccl_check = True
 
     if args.dry_run:
         return dry_run(args, rank, world, local, WORKLOADS[args.workload])
@@ -606,8 +611,8 @@ def main():
 
     # ---- single-batch latency: one batch per launch, nothing
     # else in flight; kernel time from HIP events, submit->sync on the host ----
-    n_lat = 50
-    host_us = []
+    n_lat = 0 if args.quick else 50
+    host_us = [0.0]
     ctx.launch_timing(True)
     for i in range(n_lat):
         h0 = time.perf_counter()
@@ -616,7 +621,7 @@ def main():
         host_us.append((time.perf_counter() - h0) * 1e6)
     lat_ms, _ = ctx.launch_timing_read(reset=True)
     ctx.launch_timing(False)
-    single_batch = {"batch": B, "launches": n_lat, "kernel_us_mean": round(lat_ms * 1e3, 2),
+    single_batch = None if args.quick else {"batch": B, "launches": n_lat, "kernel_us_mean": round(lat_ms * 1e3, 2),
                     "host_submit_to_sync_us_median": round(float(np.median(host_us)), 2)}
 
     # ---- the ranks' counters summed by RCCL over xGMI (print_stats' totals of
@@ -642,7 +647,7 @@ def main():
     # the same box's streaming ceiling for this byte mix (tools/ceiling.hip):
     # read every 64 B slot of the pool, write an 8 B record, nothing else
     ceiling = None
-    if not W["imix"]:
+    if not W["imix"] and not args.quick:
         ceiling = box_ceiling(res["d_pkts"].addr, P * B, res["d_res"].addr)
 
     roof = roofline_block(res, world, group, args)
@@ -692,7 +697,8 @@ def main():
         "roofline": roof,
         "cpu_baseline": None,
     }
-    out["single_batch_latency"] = single_batch
+    if single_batch:
+        out["single_batch_latency"] = single_batch
     if "pmd_info" in res:
         # the poll-mode kernel: a 1024-batch post (HBM-resident, one post, no
         # launch) timed on the host, as a fraction of the peak

@@ -101,7 +101,7 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
             }
         } else {
             // back off to ~0.5 us between polls while nothing comes
-            for (uint32_t k = spins < 16 ? 0u : 3u; k; k--) __builtin_amdgcn_s_sleep(4);
+            for (uint32_t k = spins < 16 ? 0u : P.poll_backoff; k; k--) __builtin_amdgcn_s_sleep(4);
         }
         __builtin_amdgcn_s_sleep(2);
     }

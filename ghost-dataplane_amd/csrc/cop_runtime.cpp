@@ -1902,6 +1902,8 @@ static void pmd_size(cop_pmd *m)
     // post against 16.1; 80 (stride 16) flood the link (56.8 us)
     m->P.relay_stride = 256;
     if (const char *e = getenv("COP_PMD_RELAY_STRIDE")) m->P.relay_stride = std::max(1u, (uint32_t)atoi(e));
+    m->P.poll_backoff = 3;
+    if (const char *e = getenv("COP_PMD_BACKOFF")) m->P.poll_backoff = std::min(64u, (uint32_t)atoi(e));
 }
 
 // wait for the launch's census: 0 = every worker resident, 1 = aborted

@@ -317,3 +317,30 @@ def test_dropin_error_paths_free_every_mbuf(rules_file, where):
         L.cop_ring_free(tx)
     finally:
         L.coprocessor_teardown()
+
+
+def test_no_nf_chain_forwards_everything(rules_file):
+    """process_packet without ENABLE_FW_NF forwards every packet
+    (coprocessor.c:59-64); the drop-in takes that chain from
+    cop_coprocessor_setup_stages(0) (what coprocessor_setup() expands to in
+    a build with DISABLE_NF or COP_DROPIN_NO_NF), including packets the
+    firewall would drop."""
+    path, rules = rules_file
+    L = cg.lib()
+    L.cop_set_mbuf_layout(0, 16)
+    L.cop_set_rule_file(path.encode())
+    assert L.cop_coprocessor_setup_stages(0) == 0
+    try:
+        n = 4000
+        pk = cg.gen_trace(0x5EED0510, n, rules)
+        mb = Mbufs(pk, n)
+        fwo, _ = oracle_tables(rules)
+        ro, _, _ = orc.process(pk, n, stages=DROPIN, fw=fwo)
+        assert np.sum(ro["verdict"] != 0) > 0          # the firewall would drop some
+        ptrs = (ctypes.c_void_p * n)(*[mb.ptr(i) for i in range(n)])
+        ret = np.full(n, 7, dtype=np.int32)
+        assert L.process_burst(ptrs, n, ret.ctypes.data) == 0
+        assert np.all(ret == 0)
+    finally:
+        assert L.coprocessor_teardown() == 0
+        L.cop_set_dropin_stages(cg.STAGE_FW)

@@ -239,36 +239,49 @@ extern "C" int ceiling_probe(const void *t0, const void *t1, uint32_t entries, i
     hipDeviceProp_t prop;
     if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
     if (!t0 || (tables > 1 && !t1) || entries == 0 || (entries & (entries - 1)) || iters < 1) return -1;
-    const uint32_t grid = (uint32_t)prop.multiProcessorCount * 8;
+    // shapes: 8 or 16 packets per lane in flight, 8 or 16 workgroups per
+    // CU; the best is the ceiling
+    const uint32_t ncu = (uint32_t)prop.multiProcessorCount;
     const int rounds = 4;
     uint32_t *out = nullptr;
-    if (hipMalloc(&out, (size_t)grid * 256 * 4) != hipSuccess) return -1;
+    if (hipMalloc(&out, (size_t)ncu * 16 * 256 * 4) != hipSuccess) return -1;
     hipStream_t s;
     hipEvent_t e0, e1;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return -1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -1;
-    std::vector<float> v;
     int rc = 0;
-    for (int r = 0; r <= iters; r++) {
-        (void)hipEventRecord(e0, s);
-        hipLaunchKernelGGL(probek::probe_rand<8>, dim3(grid), dim3(256), 0, s, (const uint32_t *)t0,
-                           (const uint32_t *)(tables > 1 ? t1 : t0), entries, tables, rounds,
-                           (unsigned long long)r * 0x9E3779B97F4A7C15ull, out);
-        (void)hipEventRecord(e1, s);
-        if (hipEventSynchronize(e1) != hipSuccess) {
-            rc = -1;
-            break;
+    float best = 0.f;
+    for (int shape = 0; shape < 4 && rc == 0; shape++) {
+        const int ppt = shape & 1 ? 16 : 8;
+        const uint32_t grid = ncu * (shape & 2 ? 16u : 8u);
+        std::vector<float> v;
+        for (int r = 0; r <= iters; r++) {
+            (void)hipEventRecord(e0, s);
+            if (ppt == 16)
+                hipLaunchKernelGGL(probek::probe_rand<16>, dim3(grid), dim3(256), 0, s, (const uint32_t *)t0,
+                                   (const uint32_t *)(tables > 1 ? t1 : t0), entries, tables, rounds,
+                                   (unsigned long long)r * 0x9E3779B97F4A7C15ull, out);
+            else
+                hipLaunchKernelGGL(probek::probe_rand<8>, dim3(grid), dim3(256), 0, s, (const uint32_t *)t0,
+                                   (const uint32_t *)(tables > 1 ? t1 : t0), entries, tables, rounds,
+                                   (unsigned long long)r * 0x9E3779B97F4A7C15ull, out);
+            (void)hipEventRecord(e1, s);
+            if (hipEventSynchronize(e1) != hipSuccess) {
+                rc = -1;
+                break;
+            }
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            if (r > 0) v.push_back(ms);
         }
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, e0, e1);
-        if (r > 0) v.push_back(ms);
+        if (rc == 0 && hipGetLastError() != hipSuccess) rc = -1;
+        if (rc == 0) {
+            std::sort(v.begin(), v.end());
+            const double probes = (double)grid * 256 * ppt * (tables > 1 ? 2 : 1) * rounds;
+            best = std::max(best, (float)(probes / (v[v.size() / 2] * 1e-3) / 1e9));
+        }
     }
-    if (rc == 0 && hipGetLastError() != hipSuccess) rc = -1;
-    if (rc == 0) {
-        std::sort(v.begin(), v.end());
-        const double probes = (double)grid * 256 * 8 * (tables > 1 ? 2 : 1) * rounds;
-        *gprobes_out = (float)(probes / (v[v.size() / 2] * 1e-3) / 1e9);
-    }
+    if (rc == 0) *gprobes_out = best;
     (void)hipFree(out);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);

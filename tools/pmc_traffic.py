@@ -10,6 +10,14 @@ with the pipeline's exact access pattern (kA: dword@12 + dwordx3@24 per
 64-byte slot) and with dwordx4 streaming (kD).
 
 usage: pmc_traffic.py <fetch_bench.csv> <write_bench.csv> <fetch_mb.csv> <write_mb.csv> <out.json>
+
+Every L2 read request to the fabric on gfx950 is 128 bytes, and FETCH_SIZE
+tallies each at 64 B: a streaming read makes one request per 128 B
+(tools/membench kA: 2,621,805 TCC_EA0_RDREQ for 320 MiB), and an isolated
+random dword probe one request (tools/probebench: 0.94-1.00 per probe; two
+dword loads into the two 64-byte halves of one line, issued together, merge
+into one request). So the calibrated factor 2 applies to the probe share of
+the traffic as well (profiles/r03/calib/).
 """
 import collections
 import csv
@@ -22,8 +30,14 @@ MB_SLICE = 1 << 20          # its 1 Mi-packet slice runs
 
 
 def load(path):
+    """{kernel: [(grid, value)]}; path#RDREQ / path#DRAM pick one counter of
+    a two-counter pass (TCC_EA0_RDREQ_sum / TCC_EA0_RDREQ_DRAM_sum)."""
+    path, _, which = path.partition("#")
+    want = {"RDREQ": "TCC_EA0_RDREQ_sum", "DRAM": "TCC_EA0_RDREQ_DRAM_sum"}.get(which)
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
+        if want and r["Counter_Name"] != want:
+            continue
         d[r["Kernel_Name"]].append((int(r["Grid_Size"]), float(r["Counter_Value"])))
     return d
 

@@ -17,7 +17,8 @@ for f in sys.argv[1:]:
             p = d["pmd"]
             print(f"   pmd steady {p['steady_mpkt_s']:.0f} ({p['steady_frac']}), 1-batch post {p['single_batch_post_to_done_us_median']} us, "
                   f"one-batch posts {p['one_batch_posts']['mpkt_s']:.0f}")
-        print(f"   single batch {d['single_batch_latency']}")
+        if "single_batch_latency" in d:
+            print(f"   single batch {d['single_batch_latency']}")
         for k in ("secondary", "counter_reduce", "counter_allreduce_check"):
             if k in d:
                 print(f"   {k}: {json.dumps(d[k])[:400]}")
