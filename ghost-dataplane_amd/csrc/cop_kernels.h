@@ -158,6 +158,7 @@ struct CopKPmd {
     unsigned long long idle_ticks;       // s_memrealtime ticks (100 MHz) without a post before leaving
     uint32_t n_work;                     // worker workgroups
     uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
+    uint32_t stepwise;                   // tiles step by step where tile_steps applies ($COP_PMD_STEPWISE=0: off)
     uint32_t poll_backoff;               // waiting workers' s_sleep(4) rounds between relay polls once idle
                                          // (3: ~0.3 us, the default; 0: busy polling, $COP_PMD_BACKOFF)
 };

@@ -197,9 +197,12 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             for (uint32_t i = (uint32_t)tid_i; i < p.hit_nb; i += BLOCK) lds[p.lds_hit_off + i] = 0u;
             lds_barrier();
         }
-        tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
-            p, o, lc, B, look_off, j, LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0]}, tid_i, lane_i,
-            wave_i, false, (size_t)slot * tpb + j);
+        if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && P.stepwise)
+            tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, B, j, tid_i, lane_i, wave_i);
+        else
+            tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
+                p, o, lc, B, look_off, j, LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0]}, tid_i,
+                lane_i, wave_i, false, (size_t)slot * tpb + j);
         // completion: every wave's stores (write-through) and counter adds
         // have landed, then one lane counts the tile for its slot; the slot's
         // last tile writes the batch's sequence + 1 to host memory. (One

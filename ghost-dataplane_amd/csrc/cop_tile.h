@@ -182,6 +182,97 @@ __device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &
     for (uint32_t q = (uint32_t)tid; q <= nb; q += BLOCK) st_u32<WT>(h.off[q], &p.hit_off[tile * (nb + 1) + q]);
 }
 
+// Whether a tile can run step by step (tile_steps): segmented lists, no
+// optional feature, coalesced 64-byte slots, and LDS-only lookups (no
+// global probe whose latency a per-step pass 2 would serialise).
+template <int FW, int LPM, int LAY, bool EXT>
+constexpr bool steps_ok()
+{
+    return !EXT && LAY == COPK_LAY_COALESCED && FW != COPK_TBL_DIR && LPM != COPK_TBL_DIR && LPM != COPK_TBL_TRIE;
+}
+
+// One tile of the poll-mode kernel, step by step (tile_body does the same
+// work pass by pass). The header loads of all PPT steps go out first; then
+// each step, as its loads land, is classified and finished: its records
+// (16-byte write-through stores from lane pairs), its list segment (one
+// barrier for the four waves' counts, then each forwarded lane writes its
+// index) and its segment length. The counters are folded into the last
+// step's barrier. So when a worker's last loads land (the CU serves its
+// workers' loads about in order: the last worker's after everything else),
+// one step is left to finish, not the whole tile. Same outputs as tile_body.
+template <int FW, int LPM, int PPT, bool WT>
+__device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
+                                           int tid, int lane, int wave)
+{
+    static_assert(COPK_SEG == BLOCK, "one segment per tile step");
+    const Tables &tb = lc.tb;
+    constexpr int TILE = BLOCK * PPT;
+    const uint32_t base = j * TILE;
+    const uint32_t last = B.n ? B.n - 1 : 0u;
+    const StepGeom sg = step_geom(lane);
+    u32x4 v[PPT][3];
+#pragma unroll
+    for (int k = 0; k < PPT; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
+    Counts tot;
+    uint32_t *r = (uint32_t *)B.results;
+    const int i2 = lane & 31;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        uint32_t w3[1], w6[1], w7[1], w8[1];
+        gather_step(sg, v[k], w3[0], w6[0], w7[0], w8[0]);
+        const uint32_t pk0 = base + k * BLOCK;
+        const bool valid[1] = {pk0 + tid < B.n && B.n != 0};
+        uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], src[1], dst[1], ct = 0, cn = 0;
+        pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe);
+        pass2<FW, LPM, 1>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, ct, cn);
+        const Counts c = wave_counts<FW, 1>(valid, verdict, flags);
+        tot.total += c.total;
+        tot.notv4 += c.notv4;
+        tot.fwd += c.fwd;
+        tot.dropfw += c.dropfw;
+        tot.parse += c.parse;
+        tot.noport += c.noport;
+        tot.rhit += c.rhit;
+        tot.rx += c.rx;
+        const unsigned long long bal = __ballot(valid[0] && verdict[0] == COPK_FORWARD);
+        if (lane == 0) {
+            lc.cl.cnt[k * WAVES + wave] = (uint32_t)__popcll(bal);
+            if (k == PPT - 1) {
+                const uint32_t c8[8] = {tot.total, tot.notv4, tot.fwd, tot.dropfw, tot.parse, tot.noport, tot.rhit,
+                                        tot.rx};
+#pragma unroll
+                for (int q = 0; q < 8; q++) lc.s_red[wave * 8 + q] = c8[q];
+            }
+        }
+        // records of this step: lane i < 32 stores records 2i, 2i+1 of the
+        // wave's 64 packets as one 16-byte write-through store
+        const uint32_t rx = verdict[0] | (flags[0] << 8) | (port[0] << 16);
+        const uint32_t a0 = (uint32_t)__shfl((int)rx, 2 * i2), a1 = (uint32_t)__shfl((int)rnh[0], 2 * i2);
+        const uint32_t a2 = (uint32_t)__shfl((int)rx, 2 * i2 + 1), a3 = (uint32_t)__shfl((int)rnh[0], 2 * i2 + 1);
+        const uint32_t idx = pk0 + (uint32_t)wave * 64u + 2u * (uint32_t)i2;
+        if (lane < 32) {
+            if (idx + 1 < B.n) st_u32x4<WT>(u32x4{a0, a1, a2, a3}, r, 2 * (long)idx);
+            else if (idx < B.n) st_u32x2<WT>(u32x2{a0, a1}, (u32x2 *)&r[2 * (size_t)idx]);
+        }
+        lds_barrier();
+        // the step's segment: this wave's forwarded packets after the lower
+        // waves' ones, in lane order
+        uint32_t off = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; w++) {
+            const uint32_t cw = lc.cl.cnt[k * WAVES + w];
+            off += w < wave ? cw : 0u;
+            all += cw;
+        }
+        if (B.fwd_idx && ((bal >> lane) & 1ull))
+            st_u32<WT>(pk0 + tid, &B.fwd_idx[pk0 + off +
+                                            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))]);
+        if (B.fwd_count && tid == 0 && pk0 < B.n) st_u32<WT>(all, B.fwd_count + pk0 / COPK_SEG);
+        if (k == PPT - 1) counters_add(p, lc.s_red, tid);
+    }
+}
+
 // One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,
 // parse/route, lookups, verdicts, records, ordered compaction and the
 // counter flush. Shared by the one-shot kernel (one tile per workgroup)
