@@ -571,6 +571,8 @@ def main():
     ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the value is their median")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="do not move the process onto the CPUs of the GPU's NUMA node")
     ap.add_argument("--quick", action="store_true",
                     help="A/B runs: the timed steps and the kernel roofline only (no poll-mode extras, single-batch "
                          "latency, ceilings, RCCL check, secondary workload or CPU baseline)")
@@ -602,11 +604,14 @@ def main():
     ndev = cg.device_count()
     check_devices(args, world, local, ndev)
     dev = copdist.device_for(local, ndev)
+    no_bind = args.no_numa_bind or os.environ.get("COP_NO_NUMA_BIND") == "1"
+    numa = copdist.bind_near_device(cg.device_pci_bus_id(dev)) if not no_bind else {"skipped": True}
+    log(f"[rank {rank}] host side near device {dev}: {numa}")
     group = copdist.Group(rank, world, "gloo")
 
     res, ctx = measure(args, args.workload, rank, world, dev, group, primary=True)
     W, B, P, Lb = res["W"], res["B"], res["P"], res["Lb"]
-    ranks_info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(res["own_rate"], 3),
+    ranks_info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(res["own_rate"], 3), "numa": numa,
                                    **({"rccl_init": res["coll"]} if res["rc_on"] else {})})
 
     # ---- single-batch latency: one batch per launch, nothing

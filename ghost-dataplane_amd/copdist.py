@@ -30,6 +30,40 @@ def device_for(local_rank: int, ndev: int) -> int:
     return local_rank % ndev
 
 
+def _cpulist(text: str) -> set:
+    out = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        out.update(range(int(lo), int(hi or lo) + 1))
+    return out
+
+
+def bind_near_device(pci_bus_id: str) -> dict:
+    """Run this process on the CPUs of the GPU's NUMA node (within the CPUs
+    it may use), before any pinned host buffer is allocated, so the doorbell
+    writes, completion reads and staging buffers of the host side cross no
+    socket link: the DPDK rule of placing lcores on the NIC's socket. Returns
+    what was done (reported in the bench line); never raises."""
+    info = {"pci": pci_bus_id}
+    try:
+        base = f"/sys/bus/pci/devices/{pci_bus_id}"
+        info["numa_node"] = int(open(f"{base}/numa_node").read().strip())
+        local = _cpulist(open(f"{base}/local_cpulist").read())
+        allowed = os.sched_getaffinity(0)
+        near = local & allowed
+        if near and near != allowed:
+            os.sched_setaffinity(0, near)
+            info["bound_cpus"] = len(near)
+        else:
+            info["bound_cpus"] = 0 if not near else len(near)
+        info["allowed_cpus"] = len(allowed)
+    except (OSError, ValueError) as e:
+        info["error"] = str(e)[:120]
+    return info
+
+
 def shard_seed(base: int, rank: int, index: int = 0) -> int:
     """Seed of rank `rank`'s `index`-th trace chunk: disjoint per rank."""
     return (base + 1000 * rank + index) & 0xFFFFFFFFFFFFFFFF

@@ -120,6 +120,7 @@ SIGNATURES = {
     "cop_destroy": (None, [c_void_p]),
     "cop_last_error": (c_char_p, [c_void_p]),
     "cop_device_count": (c_int, []),
+    "cop_device_pci_bus_id": (c_int, [c_int, ctypes.c_char_p, c_int]),
     "cop_set_fw_table": (c_int, [c_void_p, c_void_p]),
     "cop_set_route_lpm": (c_int, [c_void_p, c_void_p]),
     "cop_set_routing_table": (c_int, [c_void_p, c_void_p]),
@@ -437,6 +438,12 @@ def coll_unique_id() -> bytes:
 
 def device_count() -> int:
     return lib().cop_device_count()
+
+
+def device_pci_bus_id(device: int) -> str:
+    buf = ctypes.create_string_buffer(64)
+    _check(lib().cop_device_pci_bus_id(device, buf, 64), what="cop_device_pci_bus_id")
+    return buf.value.decode().lower()
 
 
 class Context:

@@ -301,6 +301,13 @@ int cop_device_count(void)
 
 const char *cop_last_error(cop_ctx *ctx) { return ctx ? ctx->err : "no context"; }
 
+int cop_device_pci_bus_id(int device, char *buf, int len)
+{
+    if (!buf || len < 13) return -EINVAL;
+    if (hipDeviceGetPCIBusId(buf, len, device) != hipSuccess) return -ENODEV;
+    return 0;
+}
+
 static void free_lpm(DevLpm &t)
 {
     if (t.starts) (void)hipFree(t.starts);

@@ -255,6 +255,10 @@ int  cop_create(const cop_config *cfg, cop_ctx **out);
 void cop_destroy(cop_ctx *ctx);
 const char *cop_last_error(cop_ctx *ctx);
 int  cop_device_count(void);
+/* PCI bus id of a device ("dddd:bb:dd.f"), so a caller can run its
+ * coprocessor threads and place their host buffers on the GPU's NUMA node
+ * (as DPDK places lcores on the NIC's socket). 0, -EINVAL or -ENODEV. */
+int  cop_device_pci_bus_id(int device, char *buf, int len);
 
 /* Upload tables (synchronous). The table may be freed afterwards. */
 int  cop_set_fw_table(cop_ctx *ctx, const cop_lpm_table *t);

@@ -60,6 +60,15 @@ def main():
         ctx.process_host(pk, 65536)
     dt = time.perf_counter() - t0
     print(f"cop_process_host (sync, 64k, incl. Python pointer list): {8 * 65536 / dt / 1e6:.1f} Mpkt/s")
+    # the CPU baseline on the same box, same run, per core count: the oracle's
+    # restatement of the reference's coprocessor() loop (bench.py's
+    # cpu_baseline), so the host paths above read per core against it
+    trace = cg.gen_trace(0x5EED0001, NB_MBUF, fw, None)
+    for cores in (1, 4, 8, 16):
+        rate, pk_n, secs = orc.coprocessor_bench(trace, NB_MBUF, o, 3.0, cores, max(os.sched_getaffinity(0)) if cores == 1
+                                                 else -1)
+        print(f"cpu baseline: restated coprocessor() loop, {cores:2d} thread(s): {rate:9.1f} Mpkt/s "
+              f"({rate / cores:.1f} per core)", flush=True)
 
 
 if __name__ == "__main__":
