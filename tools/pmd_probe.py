@@ -26,8 +26,9 @@ def main():
     ap.add_argument("--posts", default="1,20,64,128")
     ap.add_argument("--lists", default="seg", choices=("seg", "dense"))
     ap.add_argument("--dump", default="", help="save each post's raw stamps to <prefix>_post<k>.npz")
+    ap.add_argument("--rules", type=int, default=1000, help="firewall rules (fw1k: 1000)")
     args = ap.parse_args()
-    fw = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
+    fw = cg.gen_rules(0x5EED1002, args.rules, cg.GEN_FW, 20 if args.rules >= 20 else 0)
     B, P = 65536, 128
     ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, max_batch=B,
                      flags=cg.CFG_SEG_LISTS if args.lists == "seg" else 0)
@@ -41,7 +42,8 @@ def main():
     ring = cg.make_ring(dp, P, B, dr, B * 64, stride=64, fwd_idx=df, fwd_count=dc)
     m = ctx.pmd_start(ring)
     info = m.info()
-    print("pmd:", info, flush=True)
+    print("pmd:", info, "fw rules", args.rules, "intervals", ctx.fw_intervals() if hasattr(ctx, "fw_intervals") else "?",
+          flush=True)
     lib = cg.lib()
     lib.cop_debug_pmd_stamps.restype = ctypes.c_int
     lib.cop_debug_pmd_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
