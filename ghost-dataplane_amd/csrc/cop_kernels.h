@@ -152,7 +152,9 @@ struct CopKPmd {
     unsigned long long *d_posted;        // device relays of *h_posted: COPK_PMD_RELAYS copies, 128 B apart
     uint32_t *d_ctl;                     // device: [0] exit (COPK_PMD_*), [1] census, [2] look-back timeout
     unsigned long long *slot_tiles;      // per ring slot: tiles completed (multiples of tiles per batch
-                                         // between batches; zeroed at every launch)
+                                         // between batches; zeroed at every launch), slot_stride u64 apart
+    uint32_t slot_stride;                // 520 (4160 B): every counter on its own line, lines spread over
+                                         // channels (packed counters cost a 20-batch burst ~3 us: tools/burst)
     unsigned long long *stamps;          // diagnostic: s_memrealtime per worker phase (COP_PMD_STAMPS) or null
     unsigned long long seq0;             // first batch sequence this launch serves
     unsigned long long idle_ticks;       // s_memrealtime ticks (100 MHz) without a post before leaving

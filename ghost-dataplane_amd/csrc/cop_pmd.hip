@@ -213,7 +213,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
         if (tid == 0) {
-            const unsigned long long old = atomicAdd(&P.slot_tiles[slot], 1ull);
+            const unsigned long long old = atomicAdd(&P.slot_tiles[(size_t)slot * P.slot_stride], 1ull);
             if ((old + 1) % tpb == 0)
                 __hip_atomic_store(&P.h_done[slot], b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (stamp) {

@@ -2106,7 +2106,12 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         m->P.h_done = (unsigned long long *)((uint8_t *)dctl + 64);
         // device words: control and relays, slot tile counts, then the
         // look-back chains (dense lists only)
-        const size_t look_off = (PMD_CTL_BYTES + (size_t)m->n_slots * 8 + 255) & ~(size_t)255;
+        // one slot counter per 4160 bytes: 64 returning adds per batch on
+        // counters packed 16 to a line held a 20-batch burst up ~3 us
+        // (tools/burst modes 15/16, profiles/r03/burst/burst7)
+        m->P.slot_stride = 520;
+        if (const char *e = getenv("COP_PMD_SLOT_STRIDE")) m->P.slot_stride = std::max(1u, (uint32_t)atoi(e));
+        const size_t look_off = (PMD_CTL_BYTES + (size_t)m->n_slots * m->P.slot_stride * 8 + 255) & ~(size_t)255;
         const size_t look_words = (compact && !seg) ? (size_t)m->n_slots * m->tpb * (p.demux ? p.demux : 1u) : 0;
         m->dev_bytes = look_off + look_words * 8;
         if (getenv("COP_PMD_STAMPS")) {   // diagnostic phase stamps (cop_debug_pmd_stamps)

@@ -200,6 +200,11 @@ constexpr bool steps_ok()
 // step's barrier. So when a worker's last loads land (the CU serves its
 // workers' loads about in order: the last worker's after everything else),
 // one step is left to finish, not the whole tile. Same outputs as tile_body.
+// experiment builds only (timing ablations, wrong results): COPK_XP bit 1 =
+// no classification, 2 = no records, 4 = no list stores and no barrier
+#ifndef COPK_XP
+#define COPK_XP 0
+#endif
 template <int FW, int LPM, int PPT, bool WT>
 __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
                                            int tid, int lane, int wave)
@@ -223,8 +228,15 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
         const uint32_t pk0 = base + k * BLOCK;
         const bool valid[1] = {pk0 + tid < B.n && B.n != 0};
         uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], src[1], dst[1], ct = 0, cn = 0;
-        pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe);
-        pass2<FW, LPM, 1>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, ct, cn);
+        if (COPK_XP & 1) {
+            verdict[0] = (w3[0] ^ w6[0] ^ w7[0] ^ w8[0]) & 1u;
+            port[0] = w7[0] & 3u;
+            flags[0] = 0;
+            rnh[0] = w8[0];
+        } else {
+            pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe);
+            pass2<FW, LPM, 1>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, ct, cn);
+        }
         const Counts c = wave_counts<FW, 1>(valid, verdict, flags);
         tot.total += c.total;
         tot.notv4 += c.notv4;
@@ -250,9 +262,16 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
         const uint32_t a0 = (uint32_t)__shfl((int)rx, 2 * i2), a1 = (uint32_t)__shfl((int)rnh[0], 2 * i2);
         const uint32_t a2 = (uint32_t)__shfl((int)rx, 2 * i2 + 1), a3 = (uint32_t)__shfl((int)rnh[0], 2 * i2 + 1);
         const uint32_t idx = pk0 + (uint32_t)wave * 64u + 2u * (uint32_t)i2;
-        if (lane < 32) {
+        if (lane < 32 && !(COPK_XP & 2)) {
             if (idx + 1 < B.n) st_u32x4<WT>(u32x4{a0, a1, a2, a3}, r, 2 * (long)idx);
             else if (idx < B.n) st_u32x2<WT>(u32x2{a0, a1}, (u32x2 *)&r[2 * (size_t)idx]);
+        }
+        if (COPK_XP & 4) {
+            if (k == PPT - 1) {
+                lds_barrier();
+                counters_add(p, lc.s_red, tid);
+            }
+            continue;
         }
         lds_barrier();
         // the step's segment: this wave's forwarded packets after the lower

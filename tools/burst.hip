@@ -28,6 +28,7 @@
 //   mode 14 mode 0 + one returning atomic add per worker on one word, after the drain
 //   mode 15 the same on 20 words (one per batch: 64 adds each) 8 bytes apart (two lines)
 //   mode 16 mode 15 with the words 4160 bytes apart; mode 17: mode 16 without the return
+//   mode 18 mode 0 + the pipeline's counter flush (9 non-returning u64 adds into 256 packed shard lines)
 // Prints per mode the median over 15 bursts of: span (us), the p50 and p90
 // worker finish (us after the flag), and the finish by worker slot on the
 // CU (blockIdx / 256).
@@ -116,7 +117,13 @@ __global__ __launch_bounds__(256, 5) void burst(const uint8_t *__restrict__ pool
     if (MODE >= 2 && acc == 0x9E3779B9u) rec[tid] = acc;   // keeps the loads
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (MODE >= 14 && tid == 0) {
+    if (MODE == 18 && tid < 9) {
+        // the pipeline's counter flush: nine non-returning u64 adds into one
+        // of 256 counter shards, 128-byte lines packed one after another
+        unsigned long long *sh = (unsigned long long *)(ctl + 65536);
+        __hip_atomic_fetch_add(&sh[(blockIdx.x % 256) * 16 + tid], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (MODE >= 14 && MODE <= 17 && tid == 0) {
         // completion counting after the drain, as the poll-mode kernel's tiles do
         uint32_t *w = MODE == 14 ? &ctl[3] : MODE == 15 ? &ctl[64 + 2 * (blockIdx.x / 64)] : &ctl[2048 + 1040 * (blockIdx.x / 64)];
         if (MODE == 17) __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -198,7 +205,7 @@ int main()
     CHK(hipMalloc(&stamps, (G + 1) * 8));
     CHK(hipMalloc(&ctl, 1 << 20));
     std::vector<unsigned long long> h(G + 1);
-    for (int mode = 0; mode < 18; mode++) {
+    for (int mode = 0; mode < 19; mode++) {
         if (mode == 5 || (mode >= 7 && mode <= 13) || mode == 1 || mode == 3 || mode == 4) continue;   // measured: profiles/r03/burst
         std::vector<double> span, p50, p90, slot[5];
         for (int it = 0; it < 17; it++) {
@@ -222,6 +229,7 @@ int main()
             if (mode == 15) hipLaunchKernelGGL(burst<15>, dim3(G), dim3(256), 0, 0, pp, rec, ctl, stamps);
             if (mode == 16) hipLaunchKernelGGL(burst<16>, dim3(G), dim3(256), 0, 0, pp, rec, ctl, stamps);
             if (mode == 17) hipLaunchKernelGGL(burst<17>, dim3(G), dim3(256), 0, 0, pp, rec, ctl, stamps);
+            if (mode == 18) hipLaunchKernelGGL(burst<18>, dim3(G), dim3(256), 0, 0, pp, rec, ctl, stamps);
             CHK(hipGetLastError());
             CHK(hipDeviceSynchronize());
             CHK(hipMemcpy(h.data(), stamps, (G + 1) * 8, hipMemcpyDeviceToHost));
