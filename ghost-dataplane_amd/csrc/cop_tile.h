@@ -205,6 +205,9 @@ constexpr bool steps_ok()
 #ifndef COPK_XP
 #define COPK_XP 0
 #endif
+#ifndef COPK_PMD_WIN
+#define COPK_PMD_WIN 4
+#endif
 template <int FW, int LPM, int PPT, bool WT>
 __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
                                            int tid, int lane, int wave)
@@ -215,16 +218,21 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
     const uint32_t base = j * TILE;
     const uint32_t last = B.n ? B.n - 1 : 0u;
     const StepGeom sg = step_geom(lane);
-    u32x4 v[PPT][3];
+    // a window of W steps in flight: step k + W is loaded once step k is
+    // gathered, so the CU's queue holds every worker's early steps before
+    // any worker's late ones and the workers' last steps land together
+    constexpr int W = COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT;
+    u32x4 v[W][3];
 #pragma unroll
-    for (int k = 0; k < PPT; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
+    for (int k = 0; k < W; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
     Counts tot;
     uint32_t *r = (uint32_t *)B.results;
     const int i2 = lane & 31;
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         uint32_t w3[1], w6[1], w7[1], w8[1];
-        gather_step(sg, v[k], w3[0], w6[0], w7[0], w8[0]);
+        gather_step(sg, v[k % W], w3[0], w6[0], w7[0], w8[0]);
+        if (k + W < PPT) load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W]);
         const uint32_t pk0 = base + k * BLOCK;
         const bool valid[1] = {pk0 + tid < B.n && B.n != 0};
         uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], src[1], dst[1], ct = 0, cn = 0;

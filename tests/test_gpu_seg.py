@@ -184,6 +184,34 @@ def test_pmd_seg_posts_wrap(gpu_ctx_factory):
     assert ctx.counters()["rx"] == total * B
 
 
+def test_pmd_seg_prefetch_deep_posts(gpu_ctx_factory):
+    """Posts deeper than one tile per worker: every worker holds several
+    tiles of one post, so each tile prefetches its successor's headers
+    (tile_steps PF) while it finishes; posts of the whole ring, then odd
+    sizes that wrap it, with the outputs cleared in between."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    fw, _ = oracle_tables(rules)
+    B, P = 65536, 64
+    pk = cg.gen_trace(0x5EED5E64, B * P, rules)
+    rg = SegRing(ctx, pk, B, P)
+    with ctx.pmd_start(rg.ring) as m:
+        assert m.info()["workers"] * 3 < P * m.info()["tiles_per_batch"]
+        m.post(P)
+        m.wait()
+        rg.check(pk, S | F, fw)
+        rg.dr.fill(0xAB)
+        rg.dc.fill(0xFF)
+        total = P
+        for k in (33, 64, 31, 5):
+            m.post(k)
+            total += k
+        m.wait()
+        rg.check(pk, S | F, fw)
+        assert ctx.counters()["rx"] == total * B
+
+
 def test_pmd_live_snapshots_sum_exactly(gpu_ctx_factory):
     """print_stats' read-and-zero (switch.c:33-90) beside the running kernel:
     batches are posted continuously, snapshots (reset) and per-rule reads
