@@ -142,18 +142,23 @@ __device__ __forceinline__ void lds_stage(uint32_t *lds_dst, const void *gsrc, u
     }
 }
 
-// Interval search in LDS over an Eytzinger (BFS-order) tree: tree[1..m-1]
-// holds the sorted interval starts s[1..m-1] (s[0] == 0 is implicit), m a
-// power of two, padding starts 0xFFFFFFFF. Returns k = #{j >= 1 : s[j] <= ip},
-// the index of the interval holding ip. The top levels of the tree sit in
-// consecutive LDS words, so the first steps of 64 searches are broadcasts or
-// conflict-free, unlike a sorted-array search whose step-s probes all share
-// one bank.
-__device__ __forceinline__ uint32_t eyt_search(const uint32_t *tree, uint32_t levels, uint32_t ip)
+// Interval search in LDS over the bucketed form (cop_runtime.cpp
+// upload_lpm): sorted starts S[0..M), then idx[0..2^ib] (u16), idx[b] = the
+// last k with S[k] <= b << (32 - ib). The answer for ip in bucket b lies in
+// [idx[b], idx[b+1]]; binary lifting over lv levels (2^lv > the widest
+// bucket) finds the last k in it with S[k] <= ip, clamped to the bucket's
+// end (correct since S is sorted). 2 + lv dependent LDS reads.
+__device__ __forceinline__ uint32_t ivt_search(const uint32_t *S, uint32_t m, uint32_t ib, uint32_t lv, uint32_t ip)
 {
-    uint32_t i = 1;
-    for (uint32_t l = 0; l < levels; l++) i = 2u * i + (tree[i] <= ip ? 1u : 0u);
-    return i - (1u << levels);
+    const uint16_t *idx = (const uint16_t *)(S + m);
+    const uint32_t b = ip >> (32u - ib);
+    uint32_t k = idx[b];
+    const uint32_t hi = idx[b + 1];
+    for (uint32_t step = (1u << lv) >> 1; step; step >>= 1) {
+        const uint32_t c = min(k + step, hi);
+        if (S[c] <= ip) k = c;
+    }
+    return k;
 }
 
 // Decoupled look-back over one chain of tile granules (tile t at
@@ -442,8 +447,6 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
                                       uint32_t (&lpe)[PPT])
 {
     const bool stageP = (p.stages & COPK_STAGE_PARSE) != 0;
-    const uint32_t fw_lv = p.fw_m ? (uint32_t)__builtin_ctz(p.fw_m) : 0u;
-    const uint32_t lp_lv = p.lpm_m ? (uint32_t)__builtin_ctz(p.lpm_m) : 0u;
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         verdict[k] = COPK_FORWARD;
@@ -467,9 +470,9 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
         // HBM probes only for packets that reach the coprocessor (masked-off
         // lanes send no request); the others keep their stage-P verdict
         const bool reach = verdict[k] == COPK_FORWARD;
-        if (FW == COPK_TBL_IVT) fwe[k] = t.fw_v[eyt_search(t.fw_s, fw_lv, src[k])];
+        if (FW == COPK_TBL_IVT) fwe[k] = t.fw_v[ivt_search(t.fw_s, p.fw_m, p.fw_ib, p.fw_lv, src[k])];
         if (FW == COPK_TBL_DIR) fwe[k] = reach ? probe_ld(&p.fw_tbl24[src[k] >> 8], p.probe_nt) : 0u;
-        if (LPM == COPK_TBL_IVT) lpe[k] = t.lp_v[eyt_search(t.lp_s, lp_lv, dst[k])];
+        if (LPM == COPK_TBL_IVT) lpe[k] = t.lp_v[ivt_search(t.lp_s, p.lpm_m, p.lpm_ib, p.lpm_lv, dst[k])];
         if (LPM == COPK_TBL_DIR) lpe[k] = reach ? probe_ld(&p.lpm_tbl24[dst[k] >> 8], p.probe_nt) : 0u;
         if (LPM == COPK_TBL_TRIE) lpe[k] = t.lp_s[dst[k] >> 20];
     }

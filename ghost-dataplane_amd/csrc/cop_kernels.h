@@ -91,13 +91,15 @@ struct CopKParams {
     const uint32_t *rt_top;   // 256 entries: value, or 0x80000000|leaf
     const uint16_t *rt_leaf;  // nleaf * 256
     uint32_t rt_nleaf;
-    // firewall LPM
-    uint32_t fw_m;
+    // firewall LPM. Interval form in LDS: fw_starts = fw_m sorted starts,
+    // then fw_iw words of bucket index (2^fw_ib + 1 u16); fw_lv levels of
+    // binary lifting inside a bucket (cop_runtime.cpp upload_lpm)
+    uint32_t fw_m, fw_ib, fw_lv, fw_iw;
     const uint32_t *fw_starts, *fw_vals;
     const uint32_t *fw_tbl24, *fw_tbl8;
     uint32_t fw_tbl8_packed;  // tbl8 groups as packed run blocks (COPK_TBL8_PACKED form)
-    // route LPM
-    uint32_t lpm_m;
+    // route LPM (the same forms)
+    uint32_t lpm_m, lpm_ib, lpm_lv, lpm_iw;
     const uint32_t *lpm_starts, *lpm_vals;
     const uint32_t *lpm_tbl24, *lpm_tbl8;
     uint32_t lpm_tbl8_packed;

@@ -43,6 +43,10 @@ constexpr int MAX_LANES = 4;
 struct DevLpm {
     bool loaded = false;
     uint32_t m = 0;                 // padded interval count (power of two) or 0
+    // bucketed interval form: starts = sorted starts (m words) then the
+    // bucket index (iw words: 2^ib + 1 u16 first-candidate positions);
+    // lv = binary-search levels inside the widest bucket
+    uint32_t ib = 0, lv = 0, iw = 0;
     uint32_t *starts = nullptr, *vals = nullptr;
     uint32_t *tbl24 = nullptr, *tbl8 = nullptr;
     uint32_t n_ext = 0;
@@ -383,14 +387,18 @@ void cop_destroy(cop_ctx *c)
 
 static int upload_empty_ivt(cop_ctx *c, DevLpm &t)
 {
-    const uint32_t zero4[4] = {0, 0, 0, 0};
     // empty table: m = 4 (the LDS copy works in uint4 units), every value 0
-    // (miss), so whatever interval the search lands in reads nh 0, no hit
+    // (miss), so whatever interval the search lands in reads nh 0, no hit;
+    // a zero bucket index (ib 6) sends every address to interval 0
     free_lpm(t);
-    HIPCHK(c, hipMalloc(&t.starts, 16));
+    t.ib = 6;
+    t.lv = 0;
+    t.iw = ((64u + 2u) / 2u + 3u) & ~3u;
+    const std::vector<uint32_t> zeros(4 + t.iw, 0u);
+    HIPCHK(c, hipMalloc(&t.starts, zeros.size() * 4));
     HIPCHK(c, hipMalloc(&t.vals, 16));
-    HIPCHK(c, hipMemcpy(t.starts, zero4, 16, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(t.vals, zero4, 16, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(t.starts, zeros.data(), zeros.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(t.vals, zeros.data(), 16, hipMemcpyHostToDevice));
     t.m = 4;
     t.loaded = true;
     HIPCHK(c, hipDeviceSynchronize());   // the copies have landed before any lane reads them
@@ -652,35 +660,44 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
     uint32_t m = cop_lpm_form_intervals(tab, form, &s, &v);
     if (!s) return set_err(c, -ENOMEM, "interval export failed");
     if (want_ivt && m <= IVT_MAX) {
-        // Eytzinger image: tree[1..M-1] = sorted starts s[1..M-1] in BFS
-        // order (s padded with 0xFFFFFFFF, which only ip 0xFFFFFFFF reaches:
-        // its value, the last real interval's, is repeated in the pads);
-        // vals stay in sorted order, indexed by the search result.
-        uint32_t M = next_pow2(m < 4 ? 4 : m);
-        std::vector<uint32_t> sorted(M), tree(M, 0), hv(M);
+        // Bucketed form for LDS: the sorted starts (padded with 0xFFFFFFFF,
+        // which only ip 0xFFFFFFFF reaches: its value, the last real
+        // interval's, is repeated in the pads) and, per bucket of the top ib
+        // bits, the position of its first candidate (R(bucket start), R(x) =
+        // the last k with sorted[k] <= x); a lookup reads the bucket's two
+        // index entries, then binary-lifts over at most lv levels inside the
+        // bucket: 2 + lv dependent LDS reads instead of log2(M) + 1.
+        const uint32_t M = next_pow2(m < 4 ? 4 : m);
+        std::vector<uint32_t> sorted(M), hv(M);
         for (uint32_t k = 0; k < M; k++) {
             sorted[k] = k < m ? s[k] : 0xFFFFFFFFu;
             hv[k] = k < m ? v[k] : v[m - 1];
         }
-        uint32_t next = 1;
-        // iterative in-order walk of the complete tree on nodes 1..M-1
-        std::vector<uint32_t> stack;
-        uint32_t node = 1;
-        while (node < M || !stack.empty()) {
-            while (node < M) {
-                stack.push_back(node);
-                node *= 2;
-            }
-            node = stack.back();
-            stack.pop_back();
-            tree[node] = sorted[next++];
-            node = 2 * node + 1;
+        uint32_t ib = 0;
+        while ((1u << ib) < m && ib < 12) ib++;
+        if (ib < 6) ib = 6;
+        const uint32_t nb = 1u << ib, iw = ((nb + 2) / 2 + 3) & ~3u;
+        std::vector<uint32_t> img(M + iw, 0);
+        std::copy(sorted.begin(), sorted.end(), img.begin());
+        uint16_t *idx = (uint16_t *)(img.data() + M);
+        uint32_t k = 0, widest = 0;
+        for (uint32_t b = 0; b <= nb; b++) {
+            // R(b << (32 - ib)); the end sentinel is R(0xFFFFFFFF) = M - 1
+            const uint64_t x = b == nb ? 0xFFFFFFFFull : (uint64_t)b << (32 - ib);
+            while (k + 1 < M && sorted[k + 1] <= x) k++;
+            idx[b] = (uint16_t)k;
+            if (b) widest = std::max<uint32_t>(widest, idx[b] - idx[b - 1]);
         }
-        HIPCHK(c, hipMalloc(&t.starts, M * 4));
+        uint32_t lv = 0;
+        while ((1u << lv) <= widest) lv++;
+        HIPCHK(c, hipMalloc(&t.starts, (size_t)(M + iw) * 4));
         HIPCHK(c, hipMalloc(&t.vals, M * 4));
-        HIPCHK(c, hipMemcpy(t.starts, tree.data(), M * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(t.starts, img.data(), (size_t)(M + iw) * 4, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(t.vals, hv.data(), M * 4, hipMemcpyHostToDevice));
         t.m = M;
+        t.ib = ib;
+        t.lv = lv;
+        t.iw = iw;
     }
     int trc = 0;
     if (want_trie && !t.m) trc = upload_trie(c, t, s, v, m);   // too large for the LDS interval form
@@ -852,8 +869,9 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
         (p.demux || (c->cfg.flags & COP_CFG_PORT_STATS)) ? COPK_LDS_MISC_EXT_WORDS : COPK_LDS_MISC_WORDS;
     const bool stage_list = p.compact && !p.demux && (c->stage_lists || p.seg);
     auto lds_need = [&](int fwm, int lpmm) {
-        return (256u + c->rt_nleaf * 128u + (fwm == COPK_TBL_IVT ? 2u * c->fw.m : 0u) +
-                (lpmm == COPK_TBL_IVT ? 2u * c->lpm.m : lpmm == COPK_TBL_TRIE ? COPK_TRIE_L0 : 0u) + misc_words +
+        return (256u + c->rt_nleaf * 128u + (fwm == COPK_TBL_IVT ? 2u * c->fw.m + c->fw.iw : 0u) +
+                (lpmm == COPK_TBL_IVT ? 2u * c->lpm.m + c->lpm.iw : lpmm == COPK_TBL_TRIE ? COPK_TRIE_L0 : 0u) +
+                misc_words +
                 (stage_list ? COPK_BLOCK * ppt : 0u) +
                 (stage_records ? 2u * COPK_BLOCK * ppt : 0u)) *
                    4u +
@@ -868,12 +886,18 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
         else return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_need(fw_mode, lpm_mode));
     }
     p.fw_m = fw_mode == COPK_TBL_IVT ? c->fw.m : 0;
+    p.fw_ib = c->fw.ib;
+    p.fw_lv = c->fw.lv;
+    p.fw_iw = fw_mode == COPK_TBL_IVT ? c->fw.iw : 0;
     p.fw_starts = c->fw.starts;
     p.fw_vals = c->fw.vals;
     p.fw_tbl24 = c->fw.tbl24;
     p.fw_tbl8 = c->fw.tbl8;
     p.fw_tbl8_packed = c->fw.tbl8_packed ? 1u : 0u;
     p.lpm_m = lpm_mode == COPK_TBL_IVT ? c->lpm.m : 0;
+    p.lpm_ib = c->lpm.ib;
+    p.lpm_lv = c->lpm.lv;
+    p.lpm_iw = lpm_mode == COPK_TBL_IVT ? c->lpm.iw : 0;
     p.lpm_starts = c->lpm.starts;
     p.lpm_vals = c->lpm.vals;
     p.lpm_tbl24 = c->lpm.tbl24;
@@ -885,9 +909,9 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     p.lpm_tleaves = c->lpm.tleaves;
     uint32_t off = 256 + c->rt_nleaf * 128;
     p.lds_fw_off = off;
-    off += 2 * p.fw_m;
+    off += 2 * p.fw_m + p.fw_iw;
     p.lds_lpm_off = off;
-    off += lpm_mode == COPK_TBL_TRIE ? COPK_TRIE_L0 : 2 * p.lpm_m;
+    off += lpm_mode == COPK_TBL_TRIE ? COPK_TRIE_L0 : 2 * p.lpm_m + p.lpm_iw;
     p.lds_misc_off = off;
     off += misc_words;
     p.lds_stage_off = 0;

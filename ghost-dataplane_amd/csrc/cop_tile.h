@@ -44,10 +44,10 @@ __device__ __forceinline__ LdsCarve lds_carve(const CopKParams &p, uint32_t *lds
     LdsCarve c;
     c.tb.rt_top = lds;                                  // 256
     c.tb.rt_leaf = (uint16_t *)(lds + 256);       // nleaf*256 u16
-    c.tb.fw_s = lds + p.lds_fw_off;
-    c.tb.fw_v = c.tb.fw_s + p.fw_m;
+    c.tb.fw_s = lds + p.lds_fw_off;                 // sorted starts, then the bucket index
+    c.tb.fw_v = c.tb.fw_s + p.fw_m + p.fw_iw;
     c.tb.lp_s = lds + p.lds_lpm_off;
-    c.tb.lp_v = c.tb.lp_s + p.lpm_m;
+    c.tb.lp_v = c.tb.lp_s + p.lpm_m + p.lpm_iw;
     uint32_t *misc = lds + p.lds_misc_off;
     c.s_misc = misc;
     c.s_tile = misc + 32;
@@ -70,9 +70,9 @@ __device__ __forceinline__ void stage_tables(const CopKParams &p, const Tables &
     constexpr bool fw = FW == COPK_TBL_IVT, lpm = LPM == COPK_TBL_IVT, trie = LPM == COPK_TBL_TRIE;
     const StageSeg none{nullptr, nullptr, 0u};
     lds_stage_all(StageSeg{p.rt_top, tb.rt_top, 64u}, StageSeg{p.rt_leaf, (uint32_t *)tb.rt_leaf, p.rt_nleaf * 32u},
-                  fw ? StageSeg{p.fw_starts, tb.fw_s, p.fw_m >> 2} : none,
+                  fw ? StageSeg{p.fw_starts, tb.fw_s, (p.fw_m + p.fw_iw) >> 2} : none,
                   fw ? StageSeg{p.fw_vals, tb.fw_v, p.fw_m >> 2} : none,
-                  lpm ? StageSeg{p.lpm_starts, tb.lp_s, p.lpm_m >> 2}
+                  lpm ? StageSeg{p.lpm_starts, tb.lp_s, (p.lpm_m + p.lpm_iw) >> 2}
                       : trie ? StageSeg{p.lpm_tl0, tb.lp_s, COPK_TRIE_L0 / 4u} : none,
                   lpm ? StageSeg{p.lpm_vals, tb.lp_v, p.lpm_m >> 2} : none, lane, wave);
 }
