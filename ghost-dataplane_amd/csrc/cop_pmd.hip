@@ -115,8 +115,11 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
 // Workers per CU (waves per SIMD): 4 for 2048-packet tiles (<= 128 VGPRs),
 // 5 for 1024-packet tiles (<= 96), 6 for 256-packet tiles (<= 80; the SGPR
 // limit admits no more, MI355X_MICROARCH.md Residency)
+#ifndef COPK_PMD_WPE4   // experiment builds: workers per CU of the 1024-packet-tile kernel
+#define COPK_PMD_WPE4 5
+#endif
 #ifndef COPK_PMD_WAVES_PER_EU
-#define COPK_PMD_WAVES_PER_EU(ppt) ((ppt) == 8 ? 4 : (ppt) == 4 ? 5 : 6)
+#define COPK_PMD_WAVES_PER_EU(ppt) ((ppt) == 8 ? 4 : (ppt) == 4 ? COPK_PMD_WPE4 : 6)
 #endif
 template <int FW, int LPM, int LAY, int PPT, bool EXT>
 __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(const CopKPmd P)
