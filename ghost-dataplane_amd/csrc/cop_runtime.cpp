@@ -1930,8 +1930,12 @@ static void pmd_size(cop_pmd *m)
 {
     m->P.n_work = (uint32_t)m->c->ncu * m->per_cu;
     // 5 doorbell readers over PCIe: 20 (stride 64) took 17.7 us per one-batch
-    // post against 16.1; 80 (stride 16) flood the link (56.8 us)
-    m->P.relay_stride = 256;
+    // post against 16.1; 80 (stride 16) flood the link (56.8 us).
+    // Stride 257, not 256: workgroups go round-robin over the XCDs and their
+    // CUs, so every multiple of 256 lands on the same CU of XCD 0; 257 puts
+    // the five readers on five XCDs (the driver's command +2 % / +6 % in two
+    // A/B pairs, profiles/r03/lead/)
+    m->P.relay_stride = 257;
     if (const char *e = getenv("COP_PMD_RELAY_STRIDE")) m->P.relay_stride = std::max(1u, (uint32_t)atoi(e));
     m->P.poll_backoff = 3;
     m->P.stepwise = getenv("COP_PMD_STEPWISE") && !atoi(getenv("COP_PMD_STEPWISE")) ? 0u : 1u;
