@@ -1934,7 +1934,8 @@ static void pmd_size(cop_pmd *m)
     // Stride 257, not 256: workgroups go round-robin over the XCDs and their
     // CUs, so every multiple of 256 lands on the same CU of XCD 0; 257 puts
     // the five readers on five XCDs (the driver's command +2 % / +6 % in two
-    // A/B pairs, profiles/r03/lead/)
+    // A/B pairs on one box, noise on another; 16 batches in flight +15 %:
+    // profiles/r03/lead*/)
     m->P.relay_stride = 257;
     if (const char *e = getenv("COP_PMD_RELAY_STRIDE")) m->P.relay_stride = std::max(1u, (uint32_t)atoi(e));
     m->P.poll_backoff = 3;
