@@ -1,7 +1,7 @@
 """Host-side LPM builder (product setup path, cop_lpm_build) against the
 oracle's incremental restatement of DPDK rte_lpm and the brute-force LPM:
 acceptance (rte_lpm_add return codes), the accepted rule set, and the
-lookup function of both device images (Eytzinger/interval form and the
+lookup function of both device images (interval form and the
 DIR-24-8 image)."""
 import numpy as np
 import pytest
