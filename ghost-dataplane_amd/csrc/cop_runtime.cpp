@@ -679,7 +679,7 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
         const uint32_t nb = 1u << ib, iw = ((nb + 2) / 2 + 3) & ~3u;
         std::vector<uint32_t> img(M + iw, 0);
         std::copy(sorted.begin(), sorted.end(), img.begin());
-        uint16_t *idx = (uint16_t *)(img.data() + M);
+        std::vector<uint16_t> idx(nb + 1);
         uint32_t k = 0, widest = 0;
         for (uint32_t b = 0; b <= nb; b++) {
             // R(b << (32 - ib)); the end sentinel is R(0xFFFFFFFF) = M - 1
@@ -688,6 +688,7 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
             idx[b] = (uint16_t)k;
             if (b) widest = std::max<uint32_t>(widest, idx[b] - idx[b - 1]);
         }
+        memcpy(img.data() + M, idx.data(), idx.size() * sizeof(uint16_t));   // the index words (LE u16 pairs)
         uint32_t lv = 0;
         while ((1u << lv) <= widest) lv++;
         HIPCHK(c, hipMalloc(&t.starts, (size_t)(M + iw) * 4));
