@@ -365,7 +365,7 @@ def measure(args, name, rank, world, dev, group, primary):
     # the median run (median of 5 runs) ----
     pmd_on()
     run_steps(0, args.warmup)
-    runs, own_runs, reduce_runs = [], [], []
+    runs, own_runs, reduce_runs, reduce_ms = [], [], [], []
     red_tot = None
     for r in range(max(1, args.repeats)):
         pmd_on()
@@ -378,7 +378,9 @@ def measure(args, name, rank, world, dev, group, primary):
             # one reporting interval: read-and-zero the counters + per-rule
             # hits and sum them over all GPUs (RCCL beside the running
             # poll-mode kernel: an atomic exchange, then the all-reduce)
+            r0 = time.perf_counter()
             tot, _ = ctx.coll_reduce_counters(reset=True, with_rules=False)
+            reduce_ms.append((time.perf_counter() - r0) * 1e3)
             reduce_runs.append(int(tot["rx"]))
             if red_tot is None:
                 red_tot = tot   # the first interval also holds the warmup
@@ -394,7 +396,7 @@ def measure(args, name, rank, world, dev, group, primary):
     log(f"[rank {rank}] {name}: timed {args.steps} steps x {len(runs)} runs ({engine}), median "
         f"{elapsed * 1e3:.3f} ms -> {value:.1f} Mpkt/s (all ranks); runs {[round(x * 1e3, 3) for x in runs]} ms")
     res = {"W": W, "name": name, "B": B, "Lb": Lb, "P": P, "engine": engine, "value": value, "elapsed": elapsed,
-           "runs": runs, "own_rate": own_rate, "rc_on": rc_on, "coll": coll, "fw_rules": fw_rules, "routes": routes,
+           "runs": runs, "own_rate": own_rate, "reduce_ms": reduce_ms, "rc_on": rc_on, "coll": coll, "fw_rules": fw_rules, "routes": routes,
            "fw_tab": fw_tab, "rt_tab": rt_tab, "cnt_per_slot": cnt_per_slot, "d_pkts": d_pkts, "d_res": d_res,
            # every buffer the ring points at stays referenced as long as the
            # ring is used (a DeviceBuffer frees its memory when collected)
@@ -450,7 +452,9 @@ def measure(args, name, rank, world, dev, group, primary):
         n_rules = len(ctx.rule_counters())
         want = [world * (args.warmup + args.steps) * B] + [world * args.steps * B] * (len(reduce_runs) - 1)
         res["reduce_info"] = {"rccl_allreduce_u64_words": SHARD_AND_PORT_WORDS + n_rules,
-                              "ms": round(group.max(r_ms), 3), "pkts_reduced_per_interval": reduce_runs,
+                              "ms": round(group.max(r_ms), 3),
+                              "ms_per_timed_interval": [round(group.max(x), 3) for x in res["reduce_ms"]],
+                              "pkts_reduced_per_interval": reduce_runs,
                               "expected_per_interval": want, "ok": reduce_runs == want}
         if reduce_runs != want:
             log(f"[rank {rank}] RCCL interval sums {reduce_runs} differ from the packets run {want}")
@@ -540,6 +544,53 @@ def roofline_block(res, world, group, args):
     if "probe" in res:
         out["probe_bound"] = res["probe"]["probe_bound"]
         out["probe_ceiling"] = res["probe"]
+    return out
+
+
+def cpu_legs(args, W, fw_rules) -> dict:
+    """cpu_baseline (1 pinned core) and cpu_baseline_multicore (the job's CPU
+    share): the oracle's restatement of the reference coprocessor() loop
+    (oracle/cop_oracle.c) over a bounded sample, args.cpu_budget seconds."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc   # CPU baseline leg only
+    out = {}
+    ofw = orc.OracleLpm(max(1024, W["fw"]), 24 if W["fw"] <= 1000 else 1 << 20)
+    ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=W["fw"] <= 1000)
+    ns = 131072
+    trace = cg.gen_trace(0x5EED0001, ns, fw_rules, None)   # configs[0] seed: CPU reference case
+    # pin to the last core this process may use (core 0 also serves this
+    # process's main thread and the driver's interrupts)
+    core = max(os.sched_getaffinity(0))
+    rate, pk, secs = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget, 1, core)
+    model = cpu_model()
+    out["cpu_baseline"] = {
+        "value": round(rate, 3),
+        "unit": "Mpkt/s",
+        "cores": 1,
+        "kind": "port",
+        "cpu_model": model,
+        "sample": (f"{pk} packets through the restated coprocessor() loop (burst 32, 16384-slot "
+                   f"SPSC ring, 2176 B mbufs, DIR-24-8 firewall, {W['fw']} rules), "
+                   f"{secs:.1f} s on 1 pinned core (cpu {core}, {model})"),
+    }
+    log(f"[rank 0] cpu baseline {rate:.1f} Mpkt/s on 1 core ({pk} pkts)")
+    # SURVEY.md §8d (ii): one coprocessor thread per host core of this
+    # job's CPU share. The affinity mask of a GPU box lists every core of
+    # the host, but the job's share is $OMP_NUM_THREADS (16 on the pool's
+    # one-GPU boxes): the leg uses that many, and says so
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    ncores = max(1, min(affinity, share if share > 0 else affinity))
+    if ncores > 1:
+        rate_m, pk_m, secs_m = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget / 2, ncores, -1)
+        out["cpu_baseline_multicore"] = {
+            "value": round(rate_m, 3), "unit": "Mpkt/s", "cores": ncores, "kind": "port", "cpu_model": model,
+            "cores_note": (f"the job's CPU share: OMP_NUM_THREADS={share} of {affinity} cores in the affinity "
+                           f"mask" if share > 0 else f"every core of the affinity mask ({affinity})"),
+            "sample": (f"{pk_m} packets, {ncores} threads each running the restated coprocessor() loop "
+                       f"on its own rings and mbuf pool, {secs_m:.1f} s"),
+        }
+        log(f"[rank 0] cpu baseline {rate_m:.1f} Mpkt/s on {ncores} cores")
     return out
 
 
@@ -656,6 +707,10 @@ def main():
         ceiling = box_ceiling(res["d_pkts"].addr, P * B, res["d_res"].addr)
 
     roof = roofline_block(res, world, group, args)
+    # which engine the roofline's kernel time comes from (`value` may come
+    # from the poll-mode kernel: config.engine; its own roofline is
+    # roofline_pmd)
+    roof["engine"] = "launch"
     if ceiling is not None:
         roof["box_ceiling"] = {
             "what": "same pool, same process: read each 64 B slot + write an 8 B record, no classification "
@@ -710,6 +765,27 @@ def main():
         pi = res["pmd_info"]
         pi["steady_frac"] = round(pi["steady_mpkt_s"] * 1e6 * res["bytes_per_pkt"] / 1e9 / HBM_PEAK_GBS, 4)
         out["pmd"] = pi
+        # the roofline of the engine that produced `value` when it is the
+        # poll-mode kernel: algorithmic bytes of its steady 1024-batch post
+        # over the host-timed post -> done, and its PMC traffic per posted
+        # batch (a rocprofv3 pass over a kernel lifetime that served exactly
+        # K posted batches and was stopped at once: tools/pmc_pmd.py)
+        ach = pi["steady_mpkt_s"] * 1e6 * res["bytes_per_pkt"] / 1e9
+        rp = {"engine": "pmd", "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": round(ach / HBM_PEAK_GBS, 4), "batches": pi["steady_batches"], "ms": pi["steady_ms"],
+              "algorithmic_bytes_per_pkt": round(res["bytes_per_pkt"], 3), "traffic_per_batch": None,
+              "traffic_per_algorithmic": None, "traffic_source": None}
+        tp = os.path.join(TRAFFIC_DIR, f"traffic_pmd_{res['name']}_{args.lists}.json")
+        if os.path.exists(tp):
+            try:
+                tj = json.load(open(tp))
+                rp["traffic_per_batch"] = tj["hbm_bytes_per_batch"]
+                rp["traffic_per_algorithmic"] = round(tj["hbm_bytes_per_batch"] / (res["bytes_per_pkt"] * B), 4)
+                rp["traffic_source"] = (f"bench_traffic/traffic_pmd_{res['name']}_{args.lists}.json (rocprofv3 "
+                                        f"PMC over {tj.get('batches')} posted batches, tools/pmc_pmd.py)")
+            except Exception:  # noqa: BLE001
+                pass
+        out["roofline_pmd"] = rp
     if "reduce_info" in res:
         out["counter_reduce"] = res["reduce_info"]
     if allreduce_check:
@@ -732,47 +808,12 @@ def main():
             out["secondary"] = {secondary: {"error": str(e)[:300]}}
             log(f"[rank {rank}] secondary {secondary} failed: {e}")
 
-    if rank == 0 and world == 1 and not args.no_cpu:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as orc   # CPU baseline leg only
-        fw_rules = res["fw_rules"]
-        ofw = orc.OracleLpm(max(1024, W["fw"]), 24 if W["fw"] <= 1000 else 1 << 20)
-        ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=W["fw"] <= 1000)
-        ns = 131072
-        trace = cg.gen_trace(0x5EED0001, ns, fw_rules, None)   # configs[0] seed: CPU reference case
-        # pin to the last core this process may use (core 0 also serves this
-        # process's main thread and the driver's interrupts)
-        core = max(os.sched_getaffinity(0))
-        rate, pk, secs = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget, 1, core)
-        model = cpu_model()
-        out["cpu_baseline"] = {
-            "value": round(rate, 3),
-            "unit": "Mpkt/s",
-            "cores": 1,
-            "kind": "port",
-            "cpu_model": model,
-            "sample": (f"{pk} packets through the restated coprocessor() loop (burst 32, 16384-slot "
-                       f"SPSC ring, 2176 B mbufs, DIR-24-8 firewall, {W['fw']} rules), "
-                       f"{secs:.1f} s on 1 pinned core (cpu {core}, {model})"),
-        }
-        log(f"[rank 0] cpu baseline {rate:.1f} Mpkt/s on 1 core ({pk} pkts)")
-        # one coprocessor thread per host core of this
-        # job's CPU share. The affinity mask of a GPU box lists every core of
-        # the host, but the job's share is $OMP_NUM_THREADS (16 on the pool's
-        # one-GPU boxes): the leg uses that many, and says so
-        affinity = len(os.sched_getaffinity(0))
-        share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-        ncores = max(1, min(affinity, share if share > 0 else affinity))
-        if ncores > 1:
-            rate_m, pk_m, secs_m = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget / 2, ncores, -1)
-            out["cpu_baseline_multicore"] = {
-                "value": round(rate_m, 3), "unit": "Mpkt/s", "cores": ncores, "kind": "port", "cpu_model": model,
-                "cores_note": (f"the job's CPU share: OMP_NUM_THREADS={share} of {affinity} cores in the affinity "
-                               f"mask" if share > 0 else f"every core of the affinity mask ({affinity})"),
-                "sample": (f"{pk_m} packets, {ncores} threads each running the restated coprocessor() loop "
-                           f"on its own rings and mbuf pool, {secs_m:.1f} s"),
-            }
-            log(f"[rank 0] cpu baseline {rate_m:.1f} Mpkt/s on {ncores} cores")
+    # the CPU baseline: on rank 0 after the GPU timing, at
+    # every N (north_star: "next to the reference DPDK CPU coprocessor timed
+    # on the same box's host cores in the same run")
+    if rank == 0 and not args.no_cpu:
+        out.update(cpu_legs(args, W, res["fw_rules"]))
+    group.barrier()   # the other ranks wait for rank 0's CPU legs
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -820,7 +861,13 @@ def dry_run(args, rank, world, local, W):
                 "config": {"workload": args.workload, "ranks": info}}
         if reduce_info:
             line["counter_reduce"] = reduce_info
+        if not args.no_cpu:
+            # the real CPU legs (oracle), on rank 0 at every N, as in a GPU run
+            cid = W["cid"]
+            fw_rules = cg.gen_rules(0x5EED1000 + cid, W["fw"], cg.GEN_FW, 20 if W["fw"] <= 1000 else 0)
+            line.update(cpu_legs(args, W, fw_rules))
         print(json.dumps(line), flush=True)
+    group.barrier()
     group.close()
 
 

@@ -135,6 +135,12 @@ SIGNATURES = {
     "cop_pmd_run": (c_int, [c_void_p, c_uint64]),
     "cop_pmd_info": (c_int, [c_void_p, POINTER(PmdInfo)]),
     "cop_pmd_stop": (c_int, [c_void_p]),
+    "cop_pmd_start_rings": (c_int, [c_void_p, POINTER(BatchRing), c_uint32, c_uint32, POINTER(c_void_p)]),
+    "cop_pmd_post_ring": (c_int, [c_void_p, c_uint32, c_uint32]),
+    "cop_pmd_post_batch": (c_int, [c_void_p, c_uint32, c_uint32]),
+    "cop_pmd_wait_ring": (c_int, [c_void_p, c_uint32, c_uint64]),
+    "cop_pmd_posted_ring": (c_uint64, [c_void_p, c_uint32]),
+    "cop_pmd_completed_ring": (c_uint64, [c_void_p, c_uint32]),
     "cop_poll": (c_int, [c_void_p]),
     "cop_process_host": (c_int, [c_void_p, POINTER(c_void_p), c_uint32, c_void_p, c_void_p, c_void_p]),
     "cop_process_host_stream": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
@@ -172,6 +178,8 @@ SIGNATURES = {
     "cop_set_dropin_stages": (c_int, [c_uint32]),
     "cop_dropin_stages": (c_uint32, []),
     "cop_coprocessor_setup_stages": (c_int, [c_uint32]),
+    "cop_coprocessor_setup_fw": (c_int, []),
+    "cop_coprocessor_setup_no_nf": (c_int, []),
     "coprocessor_teardown": (c_int, []),
     "process_packet": (c_int, [c_void_p]),
     "process_burst": (c_int, [c_void_p, c_uint32, c_void_p]),
@@ -179,6 +187,11 @@ SIGNATURES = {
     "cop_coprocessor_poll_async": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p,
                                            POINTER(NfStats)]),
     "cop_coprocessor_flush": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, POINTER(NfStats)]),
+    "cop_pmd_host_create": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, POINTER(c_void_p)]),
+    "cop_coprocessor_poll_pmd": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p,
+                                         POINTER(NfStats)]),
+    "cop_coprocessor_flush_pmd": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, POINTER(NfStats)]),
+    "cop_pmd_host_destroy": (c_int, [c_void_p]),
     "cop_host_batch_submit": (c_int, [c_void_p, c_uint32, c_void_p, c_uint32]),
     "cop_host_batch_wait": (c_int, [c_void_p, c_uint32, POINTER(c_void_p), POINTER(c_uint32)]),
     "coprocessor_ctx": (c_void_p, []),
@@ -507,9 +520,10 @@ class Context:
     def alloc(self, nbytes) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
 
-    def pmd_start(self, ring: "BatchRing") -> "Pmd":
-        """Start the poll-mode (persistent) kernel serving `ring`."""
-        return Pmd(self, ring)
+    def pmd_start(self, ring, flags: int = 0) -> "Pmd":
+        """Start the poll-mode (persistent) kernel serving `ring` (or a list
+        of rings: one kernel serving each; PMD_VARIABLE_N in flags)."""
+        return Pmd(self, ring, flags)
 
     def submit(self, batches):
         arr = (Batch * len(batches))(*batches)
@@ -606,17 +620,36 @@ class Context:
         return ms.value, n.value
 
 
+PMD_VARIABLE_N = 1
+
+
 class Pmd:
     """A poll-mode kernel serving one batch ring (cop_pmd_*): post(count)
     hands the next `count` slots to the running kernel (batch sequence
     numbers continue across posts; batch b sits in slot b % n_slots),
-    wait(seq) blocks until batches < seq have completed."""
+    wait(seq) blocks until batches < seq have completed. With a list of
+    rings (cop_pmd_start_rings), one kernel serves them all: ring r is
+    posted and waited with post_ring / post_batch / wait_ring."""
 
-    def __init__(self, ctx: "Context", ring: "BatchRing"):
+    def __init__(self, ctx: "Context", ring, flags: int = 0):
         self.ctx = ctx
-        self.ring = ring   # keep the descriptor alive
         self.handle = c_void_p()
-        _check(lib().cop_pmd_start(ctx.handle, byref(ring), byref(self.handle)), ctx, "pmd_start")
+        if isinstance(ring, (list, tuple)):
+            arr = (BatchRing * len(ring))(*ring)
+            self.ring = arr   # keep the descriptors alive
+            self.n_rings = len(ring)
+            _check(lib().cop_pmd_start_rings(ctx.handle, arr, len(ring), flags, byref(self.handle)), ctx,
+                   "pmd_start_rings")
+        else:
+            self.ring = ring   # keep the descriptor alive
+            self.n_rings = 1
+            if flags:
+                arr = (BatchRing * 1)(ring)
+                self.ring = arr
+                _check(lib().cop_pmd_start_rings(ctx.handle, arr, 1, flags, byref(self.handle)), ctx,
+                       "pmd_start_rings")
+            else:
+                _check(lib().cop_pmd_start(ctx.handle, byref(ring), byref(self.handle)), ctx, "pmd_start")
         if not hasattr(ctx, "_pmds"):
             ctx._pmds = []
         ctx._pmds.append(self)
@@ -645,6 +678,24 @@ class Pmd:
     @property
     def posted(self) -> int:
         return int(lib().cop_pmd_posted(self.handle))
+
+    def post_ring(self, ring: int, count: int):
+        _check(lib().cop_pmd_post_ring(self.handle, ring, count), self.ctx, "pmd_post_ring")
+
+    def post_batch(self, ring: int, n: int):
+        """One batch of n packets (PMD_VARIABLE_N) to `ring`."""
+        _check(lib().cop_pmd_post_batch(self.handle, ring, n), self.ctx, "pmd_post_batch")
+
+    def wait_ring(self, ring: int, seq: int | None = None):
+        if seq is None:
+            seq = int(lib().cop_pmd_posted_ring(self.handle, ring))
+        _check(lib().cop_pmd_wait_ring(self.handle, ring, seq), self.ctx, "pmd_wait_ring")
+
+    def posted_ring(self, ring: int) -> int:
+        return int(lib().cop_pmd_posted_ring(self.handle, ring))
+
+    def completed_ring(self, ring: int) -> int:
+        return int(lib().cop_pmd_completed_ring(self.handle, ring))
 
     def info(self) -> dict:
         i = PmdInfo()

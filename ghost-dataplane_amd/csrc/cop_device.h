@@ -170,10 +170,15 @@ __device__ __forceinline__ uint32_t ivt_search(const uint32_t *S, uint32_t m, ui
 // {epoch:32, flag:2 (1 aggregate, 2 inclusive), value:30}; a stale epoch
 // counts as not ready. Spins are bounded and report through the host-mapped
 // error word. Whole wave; returns the exclusive prefix.
-// exitw (poll-mode kernel: its exit word, else null): a wait that sees it set
-// gives up without publishing, since the predecessor it waits on may belong
-// to a worker that has left; the batch is redone whole after a relaunch.
+// exitw (poll-mode kernel: its exit word, else null): a wait that sees the
+// kernel abort (COPK_PMD_ABORT) gives up without publishing, since the
+// predecessor it waits on may belong to a worker that has left, and returns
+// LB_GAVE_UP; so does a poll-mode wait that times out. A tile that gave up
+// writes no list and is not counted for its slot: the batch never completes
+// (the host sees the abort). An idle or stop exit serves every batch it has
+// let any worker start (cop_pmd.hip, the gate), so a wait there always ends.
 constexpr int LB_GROUPS = 4;
+constexpr uint32_t LB_GAVE_UP = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_t stride, uint32_t j, uint32_t agg,
                                               uint32_t epoch, uint32_t *err, int lane, const uint32_t *exitw = nullptr)
 {
@@ -221,11 +226,12 @@ __device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_
         if (consumed == 0) {
             if (++spins > (1u << 22)) {       // bounded: never hang the GPU
                 if (lane == 0) *err = 1u;
+                if (exitw) return LB_GAVE_UP; // poll mode: publish nothing, count nothing
                 break;
             }
             if (exitw && (spins & 63u) == 0 &&
-                __hip_atomic_load(exitw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                return excl;                  // the kernel is leaving: publish nothing
+                __hip_atomic_load(exitw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == COPK_PMD_ABORT)
+                return LB_GAVE_UP;            // the kernel aborts: publish nothing
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -720,6 +726,22 @@ __device__ __forceinline__ void copy_out_records(void *results, uint32_t base, u
     if ((m & 1u) && tid == 0) st_u32x2<WT>(*(const u32x2 *)&stage[2 * (m - 1)], (u32x2 *)&r[2 * (m - 1)]);
 }
 
+// One 16-byte chunk of a segment's list (words w0..w0+3 of fwd_idx, from
+// LDS). The chunk that would reach past the batch's n entries (the last
+// segment's, when its list length is not a multiple of 4) is stored word by
+// word, only its words below n: fwd_idx holds n entries, no more.
+template <bool WT>
+__device__ __forceinline__ void st_list_chunk(const uint32_t *src, uint32_t *fwd_idx, uint32_t w0, uint32_t n)
+{
+    if (w0 + 4u <= n) {
+        st_u32x4<WT>(*(const u32x4 *)src, fwd_idx, (long)w0);
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < 4u; i++)
+            if (w0 + i < n) st_u32<WT>(src[i], &fwd_idx[w0 + i]);
+    }
+}
+
 // Copy a tile's forward list (agg indices staged in LDS, in order) to
 // fwd_idx[pref ..]: 16-byte non-temporal stores on 16-byte boundaries of
 // the list, partial words only at the two ends. All BLOCK data threads.
@@ -780,8 +802,10 @@ struct CompactLds {
 // mid() runs between the look-back and the second barrier: the caller's
 // record stores go there, so the look-back's loads (vmcnt retires in order)
 // do not wait for them and the other waves store while wave 0 looks back.
+// Returns false when a look-back gave up (poll-mode abort, LB_GAVE_UP): the
+// tile then wrote no list and no count (workgroup-uniform).
 template <int PPT, bool WT, typename Mid>
-__device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, const CopKBatch &B, uint32_t lb_off,
+__device__ __forceinline__ bool compact_tile(const LookCtx &lk, const Opt &o, const CopKBatch &B, uint32_t lb_off,
                                              uint32_t j,
                                              uint32_t base, const bool (&fwd)[PPT], const uint32_t (&port)[PPT],
                                              bool seg, const CompactLds &s, int tid, int lane, int wave, Mid mid)
@@ -829,12 +853,10 @@ __device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, co
                 uint32_t c = 0;
 #pragma unroll
                 for (int w = 0; w < WAVES; w++) c += s.cnt[k * WAVES + w];
-                if (cc * 4u < c)
-                    st_u32x4<WT>(*(const u32x4 *)&s.stage[k * BLOCK + cc * 4u], B.fwd_idx,
-                                 (long)(base + k * BLOCK + cc * 4u));
+                if (cc * 4u < c) st_list_chunk<WT>(&s.stage[k * BLOCK + cc * 4u], B.fwd_idx, base + k * BLOCK + cc * 4u, B.n);
             }
         }
-        return;
+        return true;
     }
     if (!o.demux) {
         unsigned long long bal[PPT];
@@ -866,12 +888,13 @@ __device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, co
                 (o.dbg & 32u) ? j * 1024u : look_back(lk.look + lb_off, 1u, j, agg, lk.epoch, lk.err, lane, lk.exitw);
             if (lane == 0) {
                 *s.pref = excl;
-                if (B.fwd_count && j == B.ntiles - 1) st_u32<WT>(excl + agg, B.fwd_count);
+                if (B.fwd_count && j == B.ntiles - 1 && excl != LB_GAVE_UP) st_u32<WT>(excl + agg, B.fwd_count);
             }
         }
         mid();
         lds_barrier();
         const uint32_t pref = *s.pref;
+        if (pref == LB_GAVE_UP) return false;
         if (staged) {
             copy_out_list<WT>(B.fwd_idx, pref, agg, s.stage, tid);
         } else if (B.fwd_idx && !(o.dbg & 64u)) {
@@ -884,7 +907,7 @@ __device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, co
                 }
             }
         }
-        return;
+        return true;
     }
     const uint32_t K = o.demux;
 #pragma unroll
@@ -902,11 +925,13 @@ __device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, co
         const uint32_t excl = look_back(lk.look + (size_t)lb_off * K + q, K, j, agg, lk.epoch, lk.err, lane, lk.exitw);
         if (lane == 0) {
             s.dpref[q] = excl;
-            if (B.fwd_count && j == B.ntiles - 1) st_u32<WT>(excl + agg, &B.fwd_count[q]);
+            if (B.fwd_count && j == B.ntiles - 1 && excl != LB_GAVE_UP) st_u32<WT>(excl + agg, &B.fwd_count[q]);
         }
     }
     mid();
     lds_barrier();
+    for (uint32_t q = 0; q < K; q++)
+        if (s.dpref[q] == LB_GAVE_UP) return false;
     if (B.fwd_idx) {
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
@@ -924,6 +949,7 @@ __device__ __forceinline__ void compact_tile(const LookCtx &lk, const Opt &o, co
             }
         }
     }
+    return true;
 }
 
 // The tile's verdict counters as wave-uniform totals from ballots (scalar
@@ -1028,8 +1054,7 @@ __device__ __forceinline__ void seg_epilogue(const CopKParams &p, const CopKBatc
             uint32_t c = 0;
 #pragma unroll
             for (int w = 0; w < WAVES; w++) c += s.cnt[k * WAVES + w];
-            if (cc * 4u < c)
-                st_u32x4<WT>(*(const u32x4 *)&s.stage[k * BLOCK + cc * 4u], B.fwd_idx, (long)(base + k * BLOCK + cc * 4u));
+            if (cc * 4u < c) st_list_chunk<WT>(&s.stage[k * BLOCK + cc * 4u], B.fwd_idx, base + k * BLOCK + cc * 4u, B.n);
         }
     }
 }

@@ -97,6 +97,22 @@ uint32_t cop_ctx_max_batch(const cop_ctx *c);
 int cop_host_batch_submit_stages(cop_ctx *c, uint32_t stages, uint32_t slot, const void *const *pkt_data,
                                  uint32_t n);
 
+/* cop_pmd_start_rings with an explicit stage mask (the drop-in's NF chain) */
+typedef struct cop_pmd cop_pmd;
+int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t n_rings, uint32_t flags,
+                               uint32_t stages, cop_pmd **out);
+/* Mapped pinned host memory: *hptr for the host, *dptr the device's address
+ * of the same bytes (free with cop_host_free_pinned). */
+int cop_host_alloc_mapped(cop_ctx *c, size_t bytes, void **hptr, void **dptr);
+
+/* Diagnostics ($COP_HOST_PROF=1): host ns per op of the host batch paths of
+ * a context: [0] gather, [1] launch, [2] wait, [3] copy-out, [4] batches,
+ * [5] packets; and of the calling thread's drop-in ring loop:
+ * [0] drain, [1] batch call, [2] async wait, [3] forward/free, [4] calls,
+ * [5] calls with packets, [6] packets. Return the word count. */
+int cop_debug_host_prof(cop_ctx *c, uint64_t *out, uint32_t n, int reset);
+int cop_debug_dropin_prof(uint64_t *out, uint32_t n, int reset);
+
 #ifdef __cplusplus
 }
 #endif

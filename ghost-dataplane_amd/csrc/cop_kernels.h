@@ -140,25 +140,44 @@ struct CopKParams {
 #define COPK_SEG 256                 /* packets per forward-list segment (= COPK_BLOCK: one tile step) */
 
 // Poll-mode (persistent) kernel, cop_pmd.hip: n_work worker workgroups
-// serve a batch ring; every relay_stride-th one relays the host's doorbell.
+// serve n_rings batch rings (worker w serves ring w % n_rings); every
+// relay_stride-th worker of a ring relays that ring's doorbell.
+#define COPK_PMD_MAX_RINGS 8
 struct CopKPmd {
-    CopKParams k;                        // ring mode (k.rg, rg.first = 0), tables, counters,
+    CopKParams k;                        // ring mode (k.rg = ring 0, rg.first = 0), tables, counters,
                                          // options; k.uniform_ntiles = tiles per batch
-    const unsigned long long *h_posted;  // host-mapped: batches posted (monotonic)
+    // ring r (all rings: k.rg's geometry: n, n_slots, stride, layout); each
+    // ring has its own batch sequence, doorbell, gate, relays, slot counts
+    // and completion words (per-ring arrays below, ring-major)
+    CopKRing rings[COPK_PMD_MAX_RINGS];
+    unsigned long long seq0r[COPK_PMD_MAX_RINGS];   // first batch of ring r this launch serves
+    uint32_t n_rings;
+    // host-mapped [r * n_slots + slot]: the packets of the batch in that
+    // slot (variable-size batches, cop_pmd_post_batch), or null (every batch
+    // has k.rg.n packets)
+    const uint32_t *h_n;
+    unsigned long long *d_act;           // device: s_memrealtime of the last doorbell change of any ring
+    const unsigned long long *h_posted;  // host-mapped: batches posted (monotonic), ring r's at [8 r]
     const uint32_t *h_stop;              // host-mapped: non-zero = leave once idle
-    // host-mapped completion: [slot] = sequence + 1 of its last completed
-    // batch, written by the slot's last tile (every output byte of the batch,
-    // and its counter adds, landed before)
+    // host-mapped completion: [r * n_slots + slot] = sequence + 1 of its
+    // last completed batch, written by the slot's last tile (every output
+    // byte of the batch, and its counter adds, landed before)
     unsigned long long *h_done;
     uint32_t *h_state;                   // host-mapped: [0] exit reason (COPK_PMD_*), [1] census
-    unsigned long long *d_posted;        // device relays of *h_posted: COPK_PMD_RELAYS copies, 128 B apart
+    unsigned long long *d_posted;        // device relays of ring r's posted count: COPK_PMD_RELAYS copies,
+                                         // 128 B apart, ring r's at [16 (r * COPK_PMD_RELAYS + x)]
+    // device: the gate, {exit reason:8 | posted:56}. Leaders publish a posted
+    // count through it (CAS) before raising the relays; an exit closes it. Its
+    // count then bounds the batches this launch serves: every worker finishes
+    // every batch below it before leaving, none above it is started. Ring
+    // r's gate at [16 r]
+    unsigned long long *d_gate;
     uint32_t *d_ctl;                     // device: [0] exit (COPK_PMD_*), [1] census, [2] look-back timeout
-    unsigned long long *slot_tiles;      // per ring slot: tiles completed (multiples of tiles per batch
+    unsigned long long *slot_tiles;      // per (ring, slot): tiles completed (multiples of tiles per batch
                                          // between batches; zeroed at every launch), slot_stride u64 apart
     uint32_t slot_stride;                // 520 (4160 B): every counter on its own line, lines spread over
                                          // channels (packed counters cost a 20-batch burst ~3 us: tools/burst)
     unsigned long long *stamps;          // diagnostic: s_memrealtime per worker phase (COP_PMD_STAMPS) or null
-    unsigned long long seq0;             // first batch sequence this launch serves
     unsigned long long idle_ticks;       // s_memrealtime ticks (100 MHz) without a post before leaving
     uint32_t n_work;                     // worker workgroups
     uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
@@ -167,6 +186,7 @@ struct CopKPmd {
                                          // (3: ~0.3 us, the default; 0: busy polling, $COP_PMD_BACKOFF)
 };
 #define COPK_PMD_RELAYS 8
+#define COPK_PMD_GATE_SHIFT 56
 #define COPK_PMD_RUNNING 0u
 #define COPK_PMD_STOPPED 1u   /* the host asked (cop_pmd_stop) */
 #define COPK_PMD_IDLE 2u      /* no post for idle_ticks: left; the next post relaunches */

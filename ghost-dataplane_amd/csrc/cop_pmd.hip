@@ -47,41 +47,90 @@ __device__ __forceinline__ uint32_t ld_agent(uint32_t *p)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Claim the exit word (first reason wins) and tell the host.
+constexpr unsigned long long GATE_POSTED = (1ull << COPK_PMD_GATE_SHIFT) - 1ull;
+
+__device__ __forceinline__ unsigned long long ld_u64(const unsigned long long *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Publish posted count h through a ring's gate (doorbell leaders, before they
+// raise the ring's relays): false once an exit has closed it.
+__device__ __forceinline__ bool gate_publish(unsigned long long *gate, unsigned long long h)
+{
+    unsigned long long g = ld_u64(gate);
+    for (;;) {
+        if (g >> COPK_PMD_GATE_SHIFT) return false;
+        if ((g & GATE_POSTED) >= h) return true;   // another leader published as much
+        const unsigned long long seen = atomicCAS(gate, g, h);
+        if (seen == g) return true;
+        g = seen;
+    }
+}
+
+// Leave: close every ring's gate (its posted count then bounds the batches
+// of that ring served: every batch a worker may have started is finished
+// before anyone leaves, so an idle or stop exit never leaves a batch half
+// done), then claim the exit word (first reason wins; the gates are closed
+// before it is set) and tell the host.
 __device__ __forceinline__ void pmd_leave(const CopKPmd &P, uint32_t why)
 {
+    for (uint32_t r = 0; r < P.n_rings; r++) {
+        unsigned long long *gate = P.d_gate + (size_t)r * 16;
+        unsigned long long g = ld_u64(gate);
+        while (!(g >> COPK_PMD_GATE_SHIFT)) {
+            const unsigned long long seen = atomicCAS(gate, g, g | ((unsigned long long)why << COPK_PMD_GATE_SHIFT));
+            if (seen == g) break;
+            g = seen;
+        }
+    }
     if (atomicCAS(&P.d_ctl[0], 0u, why) == 0u)
         __hip_atomic_store(&P.h_state[0], why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One lane of a worker waits until batch b is posted (returns the posted
-// count) or the kernel is to leave (returns 0). Doorbell leaders (every
-// relay_stride-th worker) also read the host's counter over PCIe and raise
-// the device copy every waiting worker polls: a handful of PCIe readers,
-// not one per worker, and no workgroup slot spent on a doorbell. Leaders
-// also turn the host's stop flag, a look-back timeout or an idle spell
-// (no new post for idle_ticks) into the exit word.
-__device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd &P, unsigned long long b, bool leader)
+// One lane of a worker of ring r (its wr-th) waits until the ring's batch b
+// is posted (returns the posted count) or the kernel is to leave (returns
+// 0). After an idle or stop exit batch b is still served when it lies below
+// the closed gate's count (the returned count is then that bound). Doorbell
+// leaders (every relay_stride-th worker of the ring) also read the ring's
+// host counter over PCIe and raise the device copies every waiting worker
+// polls: a handful of PCIe readers, not one per worker, and no workgroup
+// slot spent on a doorbell. Leaders also turn the host's stop flag, a
+// look-back timeout or an idle spell (no new post on any ring for
+// idle_ticks) into the exit word.
+__device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd &P, uint32_t r, uint32_t wr,
+                                                                  unsigned long long b, bool leader)
 {
-    // this worker's copy of the relay (one 128-byte line per XCD-sized
-    // group of workers): a thousand pollers on one line would hammer one
+    // this worker's copy of the relay (one 128-byte line per group of the
+    // ring's workers): a thousand pollers on one line would hammer one
     // memory channel while other workers stream
-    unsigned long long *relay = P.d_posted + (blockIdx.x % COPK_PMD_RELAYS) * 16;
+    unsigned long long *relay = P.d_posted + ((size_t)r * COPK_PMD_RELAYS + wr % COPK_PMD_RELAYS) * 16;
+    unsigned long long *relays = P.d_posted + (size_t)r * COPK_PMD_RELAYS * 16;
+    unsigned long long *gate = P.d_gate + (size_t)r * 16;
+    const unsigned long long *h_posted = P.h_posted + (size_t)r * 8;
     unsigned long long seen = 0, t_seen = __builtin_amdgcn_s_memrealtime();
     for (uint32_t spins = 0;; spins++) {
         // every load of a poll is issued before any is used: one round trip
         // per poll, not one per load (a leader's PCIe read overlaps the rest)
-        const unsigned long long hp = __hip_atomic_load(relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long hp = ld_u64(relay);
         const uint32_t ex = ld_agent(&P.d_ctl[0]);
         unsigned long long h = 0;
-        if (leader) h = __hip_atomic_load(P.h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (leader) h = __hip_atomic_load(h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (hp > b) return hp;
-        if (ex) return 0;
+        if (ex) {
+            if (ex == COPK_PMD_ABORT) return 0;
+            // idle or stop: the gate was closed before the exit word was set
+            unsigned long long g;
+            for (uint32_t k = 0; !((g = ld_u64(gate)) >> COPK_PMD_GATE_SHIFT) && k < (1u << 20); k++)
+                __builtin_amdgcn_s_sleep(1);
+            const unsigned long long lim = g & GATE_POSTED;
+            return (g >> COPK_PMD_GATE_SHIFT) && b < lim ? lim : 0ull;
+        }
         if (leader) {
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-            if (h > hp) {
-                for (int r = 0; r < COPK_PMD_RELAYS; r++) atomicMax(P.d_posted + r * 16, h);
-                if (P.stamps) {   // diagnostic: when each doorbell value was relayed
+            if (h > hp && gate_publish(gate, h)) {
+                for (int x = 0; x < COPK_PMD_RELAYS; x++) atomicMax(relays + x * 16, h);
+                if (P.stamps && r == 0) {   // diagnostic: when each doorbell value was relayed
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2], h);
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2 + 1], now);
                 }
@@ -90,14 +139,20 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
             if (h != seen) {
                 seen = h;
                 t_seen = now;
+                if (P.n_rings > 1) atomicMax(P.d_act, now);   // activity on this ring keeps every ring's kernel up
             }
             // the exit checks every 16th poll: the stop flag is a second
             // PCIe read, and the doorbell is polled once per round trip
             if ((spins & 15u) == 15u) {
-                if (ld_agent(&P.d_ctl[2])) pmd_leave(P, COPK_PMD_ABORT);   // a look-back timed out
-                else if (__hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+                if (ld_agent(&P.d_ctl[2])) {
+                    pmd_leave(P, COPK_PMD_ABORT);   // a look-back timed out
+                } else if (__hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
                     pmd_leave(P, COPK_PMD_STOPPED);
-                else if (now - t_seen > P.idle_ticks) pmd_leave(P, COPK_PMD_IDLE);
+                } else {
+                    unsigned long long last = t_seen;
+                    if (P.n_rings > 1) last = max(last, ld_u64(P.d_act));
+                    if (now - last > P.idle_ticks) pmd_leave(P, COPK_PMD_IDLE);
+                }
             }
         } else {
             // back off to ~0.5 us between polls while nothing comes
@@ -105,6 +160,25 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
         }
         __builtin_amdgcn_s_sleep(2);
     }
+}
+
+// Batch descriptor of ring rg's slot with n packets (pmd rings: ring mode)
+__device__ __forceinline__ __attribute__((unused)) CopKBatch pmd_batch(const CopKParams &p, const CopKRing &rg, uint32_t slot, uint32_t n,
+                                               uint32_t ntiles)
+{
+    CopKBatch B;
+    B.pkts = rg.pkts + (size_t)slot * rg.pkts_slot_bytes;
+    B.offsets = rg.offsets ? rg.offsets + (size_t)slot * rg.offsets_slot_words : nullptr;
+    B.results = (uint2 *)rg.results + (size_t)slot * rg.results_slot;
+    B.fwd_idx = rg.fwd_idx ? rg.fwd_idx + (size_t)slot * rg.fwd_slot : nullptr;
+    // counts per slot: one, one per port (demux), or one per segment
+    const uint32_t per = p.seg ? (rg.n + COPK_SEG - 1u) / COPK_SEG : p.demux ? p.demux : 1u;
+    B.fwd_count = rg.fwd_count ? rg.fwd_count + (size_t)slot * per : nullptr;
+    B.n = n;
+    B.stride = rg.stride;
+    B.data_off = rg.data_off;
+    B.ntiles = ntiles;
+    return B;
 }
 
 // experiment builds only: COPK_PMD_WT=0 stores non-temporally (timing of the
@@ -131,7 +205,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
     const Opt o = EXT ? opt_all(p) : Opt{0u, 0u, 0u, nullptr};
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const LdsCarve lc = lds_carve<PPT>(p, lds);
-    uint32_t *s_door = lc.s_misc + 36;   // [0..1] posted, [2] leave
+    uint32_t *s_door = lc.s_misc + 36;   // [0..1] posted, [2] leave, [3] the batch's packets
     stage_tables<FW, LPM>(p, lc.tb, lane, wave);
 
     // census: every worker and the doorbell resident, or nobody works
@@ -153,22 +227,29 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         __hip_atomic_store(&P.h_state[1], P.n_work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 
     const uint32_t tpb = p.uniform_ntiles;
-    const uint32_t G = P.n_work;
     const uint32_t n_slots = p.rg.n_slots;
-    // tile (b, j, slot) of T = seq0*tpb + blockIdx.x, advanced by G per step
-    unsigned long long b = P.seq0 + blockIdx.x / tpb;
-    uint32_t j = blockIdx.x % tpb;
+    constexpr uint32_t TILE = BLOCK * PPT;
+    // this worker's ring and its index among the ring's G workers
+    const uint32_t R = P.n_rings;
+    const uint32_t r = __builtin_amdgcn_readfirstlane(blockIdx.x % R);
+    const uint32_t wr = blockIdx.x / R;
+    const uint32_t G = (P.n_work - r + R - 1) / R;
+    const CopKRing &rg = P.rings[r];
+    const uint32_t rs0 = r * n_slots;   // ring r's first (slot-count, completion, n) word
+    // tile (b, j, slot) of T = seq0r[r]*tpb + wr, advanced by G per step
+    unsigned long long b = P.seq0r[r] + wr / tpb;
+    uint32_t j = wr % tpb;
     uint32_t slot = (uint32_t)(b % n_slots);
     const uint32_t qb = G / tpb, rb = G % tpb;
     unsigned long long posted = 0;
-    const bool leader = blockIdx.x % P.relay_stride == 0;
+    const bool leader = wr % P.relay_stride == 0;
     unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
     for (;;) {
         if (stamp && tid == 0) st_stamp(&stamp[0], __builtin_amdgcn_s_memrealtime());   // diagnostic: tile start
         if (b >= posted) {
             // wait for batch b to be posted (one lane polls the relay)
             if (tid == 0) {
-                const unsigned long long hp = wait_posted(P, b, leader);
+                const unsigned long long hp = wait_posted(P, r, wr, b, leader);
                 s_door[0] = (uint32_t)hp;
                 s_door[1] = (uint32_t)(hp >> 32);
                 s_door[2] = hp == 0 ? 1u : 0u;
@@ -183,6 +264,17 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             st_stamp(&stamp[1], __builtin_amdgcn_s_memrealtime());   // batch b posted (as seen here)
             st_stamp(&stamp[4], b);
         }
+        // the batch's packets: fixed (the ring's n), or the host's count for
+        // the slot (written before the doorbell that posted the batch)
+        uint32_t n = rg.n;
+        if (P.h_n) {
+            if (tid == 0)
+                s_door[3] = __hip_atomic_load(&P.h_n[rs0 + slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            lds_barrier();
+            n = min(s_door[3], rg.n);
+            lds_barrier();
+        }
+        const uint32_t ntiles = (n + TILE - 1) / TILE;
         // The lane's index is made opaque each iteration, so the per-lane
         // values the tile derives from it (load geometry, LDS addresses) are
         // recomputed in the tile rather than hoisted out of the loop and held
@@ -192,20 +284,25 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         asm volatile("" : "+v"(tid_i));
         const int lane_i = tid_i & 63;
         const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
-        uint32_t look_off;
-        const CopKBatch B = batch_desc(p, slot, &look_off);
-        if (EXT && p.hit_region) {
-            // binned rule hits: the tile's bucket counts start at zero (the
-            // last tile's sort is done with them: the barrier below ordered it)
-            for (uint32_t i = (uint32_t)tid_i; i < p.hit_nb; i += BLOCK) lds[p.lds_hit_off + i] = 0u;
-            lds_barrier();
+        const uint32_t look_off = (rs0 + slot) * tpb;
+        const CopKBatch B = pmd_batch(p, rg, slot, n, ntiles);
+        bool ok = true;
+        if (j < ntiles) {   // (a tile past a short batch's packets has nothing to do)
+            if (EXT && p.hit_region) {
+                // binned rule hits: the tile's bucket counts start at zero (the
+                // last tile's sort is done with them: the barrier below ordered it)
+                for (uint32_t i = (uint32_t)tid_i; i < p.hit_nb; i += BLOCK) lds[p.lds_hit_off + i] = 0u;
+                lds_barrier();
+            }
+            // tile_steps stores records from lane pairs only (p.rec_paired: every
+            // slot's records 16-byte aligned); other record forms take tile_body
+            if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && p.rec_paired && P.stepwise)
+                tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, B, j, tid_i, lane_i, wave_i);
+            else
+                ok = tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
+                    p, o, lc, B, look_off, j, LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0]}, tid_i,
+                    lane_i, wave_i, false, (size_t)(rs0 + slot) * tpb + j);
         }
-        if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && P.stepwise)
-            tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, B, j, tid_i, lane_i, wave_i);
-        else
-            tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
-                p, o, lc, B, look_off, j, LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0]}, tid_i,
-                lane_i, wave_i, false, (size_t)slot * tpb + j);
         // completion: every wave's stores (write-through) and counter adds
         // have landed, then one lane counts the tile for its slot; the slot's
         // last tile writes the batch's sequence + 1 to host memory. (One
@@ -215,10 +312,12 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
-        if (tid == 0) {
-            const unsigned long long old = atomicAdd(&P.slot_tiles[(size_t)slot * P.slot_stride], 1ull);
+        // (a tile whose look-back gave up, ok false, is not counted: its
+        // batch never completes and the host sees the abort)
+        if (tid == 0 && ok) {
+            const unsigned long long old = atomicAdd(&P.slot_tiles[(size_t)(rs0 + slot) * P.slot_stride], 1ull);
             if ((old + 1) % tpb == 0)
-                __hip_atomic_store(&P.h_done[slot], b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&P.h_done[rs0 + slot], b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (stamp) {
                 st_stamp(&stamp[3], __builtin_amdgcn_s_memrealtime());   // stores drained, tile counted
                 st_stamp(&stamp[5], (old + 1) % tpb == 0 ? 1ull : 0ull);

@@ -243,7 +243,18 @@ struct cop_ctx {
     size_t tele_words = 0;
     unsigned long long *ctr_snap = nullptr;   // cop_coll_reduce_counters(reset): exchanged words
     size_t ctr_snap_words = 0;
+    // host-path op times ($COP_HOST_PROF=1, cop_debug_host_prof): gather,
+    // launch, wait, copy-out ns; batches; packets
+    bool hprof = false;
+    uint64_t hp[6] = {0, 0, 0, 0, 0, 0};
 };
+
+static inline uint64_t hp_ns()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 static int set_err(cop_ctx *c, int code, const char *fmt, ...)
 {
@@ -504,6 +515,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_LOADS")) c->coalesced = strcmp(e, "strided") != 0;
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
     if (const char *e = getenv("COP_HIT_BINS")) c->hit_bins = atoi(e) != 0;
+    if (const char *e = getenv("COP_HOST_PROF")) c->hprof = atoi(e) != 0;
     if (const char *e = getenv("COP_STATIC_ORDER")) c->static_small = atoi(e) != 0;
     if (const char *e = getenv("COP_REC_PAIRED")) c->rec_paired = atoi(e) != 0;
     if (const char *e = getenv("COP_PROBE_NT")) c->probe_nt = atoi(e) != 0;
@@ -1231,7 +1243,13 @@ static int process_host_zc(cop_ctx *c, uint32_t stages, const void *const *pkt_d
         c->zc_cap = cap;
     }
     if (int rc0 = sync_lanes(c)) return rc0;   // the mapped buffers may still be in use
+    uint64_t t0 = c->hprof ? hp_ns() : 0;
     host_gather(c, pkt_data, c->zc_stage, n);
+    if (c->hprof) {
+        const uint64_t t1 = hp_ns();
+        c->hp[0] += t1 - t0;
+        t0 = t1;
+    }
     void *d_stage = nullptr, *d_res = nullptr, *d_fwd = nullptr;
     HIPCHK(c, hipHostGetDevicePointer(&d_stage, c->zc_stage, 0));
     HIPCHK(c, hipHostGetDevicePointer(&d_res, c->zc_res, 0));
@@ -1245,11 +1263,26 @@ static int process_host_zc(cop_ctx *c, uint32_t stages, const void *const *pkt_d
     b.fwd_idx = fwd_idx ? (uint32_t *)d_fwd + 4 : nullptr;
     b.fwd_count = (fwd_idx || fwd_count) ? (uint32_t *)d_fwd : nullptr;
     if (int rc = submit_on(c, c->lane[0], &b, 1, false, stages)) return rc;
+    if (c->hprof) {
+        const uint64_t t1 = hp_ns();
+        c->hp[1] += t1 - t0;
+        t0 = t1;
+    }
     if (int rc = cop_sync(c)) return rc;
+    if (c->hprof) {
+        const uint64_t t1 = hp_ns();
+        c->hp[2] += t1 - t0;
+        t0 = t1;
+    }
     memcpy(results, c->zc_res, (size_t)n * sizeof(cop_result));
     const uint32_t cnt = b.fwd_count ? c->zc_fwd[0] : 0u;
     if (fwd_idx && cnt) memcpy(fwd_idx, c->zc_fwd + 4, (size_t)cnt * 4);
     if (fwd_count) *fwd_count = cnt;
+    if (c->hprof) {
+        c->hp[3] += hp_ns() - t0;
+        c->hp[4]++;
+        c->hp[5] += n;
+    }
     return 0;
 }
 
@@ -1363,7 +1396,13 @@ int cop_host_batch_submit_stages(cop_ctx *c, uint32_t stages, uint32_t slot, con
     h.n = n;
     if (n) {
         // the 16-byte header records into mapped memory, then the pipeline
+        uint64_t t0 = c->hprof ? hp_ns() : 0;
         host_gather(c, pkt_data, h.h_stage, n);
+        if (c->hprof) {
+            const uint64_t t1 = hp_ns();
+            c->hp[0] += t1 - t0;
+            t0 = t1;
+        }
         cop_batch b;
         memset(&b, 0, sizeof(b));
         b.pkts = h.d_stage;
@@ -1371,6 +1410,11 @@ int cop_host_batch_submit_stages(cop_ctx *c, uint32_t stages, uint32_t slot, con
         b.stride = COP_HDR16_STRIDE;
         b.results = h.d_res;
         if (int rc = submit_on(c, L, &b, 1, false, stages)) return rc;
+        if (c->hprof) {
+            c->hp[1] += hp_ns() - t0;
+            c->hp[4]++;
+            c->hp[5] += n;
+        }
     }
     HIPCHK(c, hipEventRecord(h.done, L.s));
     h.busy = true;
@@ -1382,7 +1426,9 @@ int cop_host_batch_wait(cop_ctx *c, uint32_t slot, const cop_result **results, u
     if (!c || slot >= COP_HOST_SLOTS) return -EINVAL;
     auto &h = c->hs[slot];
     if (!h.busy) return set_err(c, -EINVAL, "host slot %u has no batch", slot);
+    const uint64_t t0 = c->hprof ? hp_ns() : 0;
     hipError_t e = hipEventSynchronize(h.done);
+    if (c->hprof) c->hp[2] += hp_ns() - t0;
     if (c->inject_wait) {
         c->inject_wait--;
         e = hipErrorUnknown;
@@ -1656,6 +1702,22 @@ int cop_coll_init(cop_ctx *c, const uint8_t id[COP_COLL_ID_BYTES], int rank, int
         c->comm = nullptr;
         return set_err(c, -EIO, "ncclCommInitRank: %s", g_rccl.error_string(r));
     }
+    // one all-reduce of a single word now (every rank is in this call): the
+    // communicator's lazy set-up and its kernels' first dispatch happen here,
+    // not in the first reporting interval beside a running poll-mode kernel
+    // ($COP_COLL_PREWARM=0: off, experiments)
+    const char *pw = getenv("COP_COLL_PREWARM");
+    if (pw && !atoi(pw)) return 0;
+    if (c->ctr_sum_words < 1) {
+        if (c->ctr_sum) (void)hipFree(c->ctr_sum);
+        c->ctr_sum = nullptr;
+        c->ctr_sum_words = 0;
+        HIPCHK(c, hipMalloc(&c->ctr_sum, 8));
+        c->ctr_sum_words = 1;
+    }
+    r = g_rccl.all_reduce(c->counters, c->ctr_sum, 1, ncclUint64, ncclSum, c->comm, c->stream);
+    if (r != ncclSuccess) return set_err(c, -EIO, "ncclAllReduce: %s", g_rccl.error_string(r));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return 0;
 }
 
@@ -1731,6 +1793,20 @@ int cop_host_alloc_pinned(cop_ctx *c, size_t bytes, void **hptr)
     return 0;
 }
 
+int cop_host_alloc_mapped(cop_ctx *c, size_t bytes, void **hptr, void **dptr)
+{
+    if (!c || !hptr || !dptr) return -EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocMapped));
+    hipError_t e = hipHostGetDevicePointer(dptr, *hptr, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(*hptr);
+        *hptr = nullptr;
+        return set_err(c, -EIO, "mapping: %s", hipGetErrorString(e));
+    }
+    return 0;
+}
+
 int cop_host_free_pinned(cop_ctx *c, void *hptr)
 {
     if (!c) return -EINVAL;
@@ -1803,10 +1879,15 @@ int cop_timer_stop(cop_ctx *c, double *ms)
 
 
 // ---- poll-mode kernel (cop_pmd.hip) ---------------------------------------
-// A persistent kernel serving one batch ring: the host posts batches by
-// bumping a counter in mapped host memory and reads their completion from
-// per-slot words the kernel writes there. No launch, no per-launch ramp,
-// tables staged into LDS once per worker.
+// A persistent kernel serving one or several batch rings: the host posts a
+// ring's batches by bumping its counter in mapped host memory and reads
+// their completion from per-slot words the kernel writes there. No launch,
+// no per-launch ramp, tables staged into LDS once per worker.
+
+struct PmdRing {
+    std::atomic<uint64_t> posted{0};      // batches posted (written by the ring's thread)
+    std::atomic<uint64_t> completed{0};   // first batch not known complete (the ring's thread)
+};
 
 struct cop_pmd {
     cop_ctx *c = nullptr;
@@ -1815,45 +1896,67 @@ struct cop_pmd {
     int fw_mode = 0, lpm_mode = 0, layout = 0, ppt = 0, ext = 0;
     uint32_t lds_bytes = 0;
     uint8_t *ctl = nullptr;                 // mapped host control block
-    volatile uint64_t *h_posted = nullptr;
     volatile uint32_t *h_stop = nullptr;
     volatile uint32_t *h_state = nullptr;
-    volatile uint64_t *h_done = nullptr;    // [slot]: sequence + 1 of its last completed batch
-    uint8_t *dev = nullptr;                 // device words: relays, ctl, slot tile counts, look-back
+    volatile uint64_t *h_done = nullptr;    // [r * n_slots + slot]: sequence + 1 of its last completed batch
+    volatile uint32_t *h_n = nullptr;       // [r * n_slots + slot]: packets of the posted batch (variable n)
+    uint8_t *dev = nullptr;                 // device words: ctl, gates, relays, slot tile counts, look-back
     size_t dev_bytes = 0;
-    uint64_t posted = 0, completed = 0;
-    uint32_t n_slots = 0, tpb = 0, per_cu = 0;
-    uint32_t launches = 0;
+    uint32_t n_rings = 1, n_slots = 0, tpb = 0, per_cu = 0, ring_n = 0;
+    std::atomic<uint32_t> launches{0};
     bool live = false;                      // a launch may still be running
-    // per-rule hits by binning: tile (slot, j) parks its sorted hit ids in
-    // region slot*tpb + j; cop_hit_count adds them up on stream hs, over
-    // runs of completed batches, before their slots are posted again
+    std::mutex mu;                          // relaunch after an idle exit, from any ring's thread
+    PmdRing ring[COPK_PMD_MAX_RINGS];
+    // per-rule hits by binning (one ring only): tile (slot, j) parks its
+    // sorted hit ids in region slot*tpb + j; cop_hit_count adds them up on
+    // stream hs, over runs of completed batches, before their slots are
+    // posted again
     bool bins = false;
     hipStream_t hs = nullptr;
     uint64_t counted = 0;                   // batches < counted have their count launched
     uint64_t count_synced = 0;              // ... and completed
+    volatile uint64_t *h_posted(uint32_t r) const { return (volatile uint64_t *)(ctl + 64 * (size_t)r); }
 };
 
-// device words: [8] d_ctl, [256 + 128 r] relay r, then the slot tile counts,
-// then the look-back chains (dense lists)
-constexpr size_t PMD_RELAY_OFF = 256;
-constexpr size_t PMD_CTL_BYTES = PMD_RELAY_OFF + 128 * COPK_PMD_RELAYS;
+// host control block: [64 r] ring r's posted count, [512] stop, [516] state
+// words, [576] the completion words, then the batch sizes (variable n)
+constexpr size_t PMD_H_STOP = 512, PMD_H_STATE = 516, PMD_H_DONE = 576;
+// device words: [8] d_ctl, [64] d_act, [1024 + 128 r] ring r's gate,
+// [2048 + 128 (8 r + x)] its relays, then the slot tile counts, then the
+// look-back chains (dense lists)
+constexpr size_t PMD_ACT_OFF = 64;
+constexpr size_t PMD_GATE_OFF = 1024;
+constexpr size_t PMD_RELAY_OFF = 2048;
+constexpr size_t PMD_CTL_BYTES = PMD_RELAY_OFF + 128 * COPK_PMD_RELAYS * COPK_PMD_MAX_RINGS;
+static_assert(PMD_GATE_OFF + 128 * COPK_PMD_MAX_RINGS <= PMD_RELAY_OFF, "gates overlap relays");
+static_assert(64 * COPK_PMD_MAX_RINGS <= PMD_H_STOP, "posted words overlap the stop word");
 
-static int pmd_launch(cop_pmd *m, uint64_t seq0)
+// the first batch of ring r not complete, from the completion words (a scan
+// from what the ring's thread last saw; it never passes a batch not posted)
+static uint64_t pmd_scan(const cop_pmd *m, uint32_t r)
+{
+    uint64_t c = m->ring[r].completed.load(std::memory_order_relaxed);
+    const volatile uint64_t *d = m->h_done + (size_t)r * m->n_slots;
+    while (d[c % m->n_slots] == c + 1) c++;
+    return c;
+}
+
+static int pmd_launch(cop_pmd *m)
 {
     cop_ctx *c = m->c;
     HIPCHK(c, hipSetDevice(c->device));
-    // every device word restarts at zero: relays, exit and census words,
-    // the slot tile counts and the look-back chains. A launch that left idle
-    // may have left a batch half done (a post raced the idle exit): that
-    // batch is redone whole by this launch, so neither its partial tile
-    // count nor its granules (whose epoch tags would match) may survive.
+    // every device word restarts at zero: the gates, relays, exit and census
+    // words, the slot tile counts and the look-back chains. An idle exit
+    // leaves no batch half done (the gates: every batch a worker may have
+    // started is finished before the workers leave, so each tile's counter
+    // and per-rule adds happen exactly once); this launch serves each ring
+    // from its first batch not completed.
     HIPCHK(c, hipMemsetAsync(m->dev, 0, m->dev_bytes, m->s));
     m->h_state[0] = 0;
     m->h_state[1] = 0;
     *m->h_stop = 0;
+    for (uint32_t r = 0; r < m->n_rings; r++) m->P.seq0r[r] = pmd_scan(m, r);
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    m->P.seq0 = seq0;
     hipError_t e = copk_pmd_launch(&m->P, m->fw_mode, m->lpm_mode, m->layout, m->ppt, m->ext, m->lds_bytes, m->s);
     if (e != hipSuccess) return set_err(c, -EIO, "pmd launch: %s", hipGetErrorString(e));
     m->launches++;
@@ -1879,22 +1982,29 @@ static int pmd_join(cop_pmd *m, double timeout_s)
     return 0;
 }
 
-// advance m->completed over the slots' completion words
-static void pmd_refresh(cop_pmd *m)
+// advance ring r's completed count over its completion words (the ring's thread)
+static uint64_t pmd_refresh(cop_pmd *m, uint32_t r = 0)
 {
-    while (m->completed < m->posted && m->h_done[m->completed % m->n_slots] == m->completed + 1) m->completed++;
+    PmdRing &g = m->ring[r];
+    const uint64_t posted = g.posted.load(std::memory_order_relaxed);
+    uint64_t c = g.completed.load(std::memory_order_relaxed);
+    const volatile uint64_t *d = m->h_done + (size_t)r * m->n_slots;
+    while (c < posted && d[c % m->n_slots] == c + 1) c++;
+    g.completed.store(c, std::memory_order_relaxed);
+    return c;
 }
 
 // count the binned rule hits of every completed batch not yet counted
 // (cop_hit_count over runs of consecutive slots, on stream hs, beside the
-// running kernel)
+// running kernel; one ring)
 static int pmd_hits_launch(cop_pmd *m)
 {
     if (!m->bins) return 0;
     const CopKParams &p = m->P.k;
-    while (m->counted < m->completed) {
+    const uint64_t completed = m->ring[0].completed.load(std::memory_order_relaxed);
+    while (m->counted < completed) {
         const uint32_t s0 = (uint32_t)(m->counted % m->n_slots);
-        const uint32_t k = (uint32_t)std::min<uint64_t>(m->completed - m->counted, m->n_slots - s0);
+        const uint32_t k = (uint32_t)std::min<uint64_t>(completed - m->counted, m->n_slots - s0);
         CopKParams q = p;
         q.hit_region = p.hit_region + (size_t)s0 * m->tpb * p.hit_reg_words;
         q.hit_off = p.hit_off + (size_t)s0 * m->tpb * (p.hit_nb + 1);
@@ -1920,8 +2030,7 @@ static int pmd_hits_flush(cop_ctx *c)
 {
     cop_pmd *m = c->pmd;
     if (!m || !m->bins) return 0;
-    pmd_refresh(m);
-    return pmd_hits_sync(m, m->completed);
+    return pmd_hits_sync(m, pmd_refresh(m, 0));
 }
 
 // every worker must be resident at once (static tile order): all of the
@@ -1936,7 +2045,8 @@ static void pmd_size(cop_pmd *m)
     // CUs, so every multiple of 256 lands on the same CU of XCD 0; 257 puts
     // the five readers on five XCDs (the driver's command +2 % / +6 % in two
     // A/B pairs on one box, noise on another; 16 batches in flight +15 %:
-    // profiles/r03/lead*/)
+    // profiles/r03/lead*/). With several rings each ring's worker 0 reads
+    // its ring's doorbell (one reader per ring).
     m->P.relay_stride = 257;
     if (const char *e = getenv("COP_PMD_RELAY_STRIDE")) m->P.relay_stride = std::max(1u, (uint32_t)atoi(e));
     m->P.poll_backoff = 3;
@@ -1959,18 +2069,48 @@ static int pmd_census(cop_pmd *m)
     }
 }
 
-// Launch serving from seq0 with every worker resident: when the census finds
-// workers that could not become resident (another kernel, context or process
-// holds CUs, likely after an idle exit), retry with one worker fewer per CU.
-static int pmd_launch_resident(cop_pmd *m, uint64_t seq0)
+// Dispatch every side kernel that may have to run beside the persistent
+// kernel once on its own stream, before the persistent kernel holds the CUs:
+// the binned hit count (stream hs) and the counter snapshot (telemetry and
+// context streams). Their code objects are then loaded and their queues set
+// up while the GPU is free. ($COP_PMD_PREWARM=0: off, experiments)
+static int pmd_prewarm(cop_pmd *m)
+{
+    cop_ctx *c = m->c;
+    const char *env = getenv("COP_PMD_PREWARM");
+    if (env && !atoi(env)) return 0;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (m->bins) {
+        hipError_t e = copk_hit_count(&m->P.k, 0, COPK_BLOCK * (uint32_t)m->ppt, m->hs);
+        if (e != hipSuccess) return set_err(c, -EIO, "pmd prewarm: %s", hipGetErrorString(e));
+        HIPCHK(c, hipStreamSynchronize(m->hs));
+    }
+    if (!c->tele_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->tele_stream, hipStreamNonBlocking));
+    if (!c->tele_dev) {
+        HIPCHK(c, hipMalloc(&c->tele_dev, 8));
+        c->tele_words = 1;
+    }
+    for (hipStream_t s : {c->tele_stream, c->stream}) {
+        hipError_t e = copk_snapshot(c->counters, 1, c->tele_dev, 0, s);
+        if (e != hipSuccess) return set_err(c, -EIO, "pmd prewarm: %s", hipGetErrorString(e));
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    return 0;
+}
+
+// Launch with every worker resident: when the census finds workers that
+// could not become resident (another kernel, context or process holds CUs,
+// likely after an idle exit), retry with one worker fewer per CU.
+static int pmd_launch_resident(cop_pmd *m)
 {
     for (;;) {
-        if (int rc = pmd_launch(m, seq0)) return rc;
+        if (int rc = pmd_launch(m)) return rc;
         const int st = pmd_census(m);
         if (st == 0) return 0;
         if (st < 0) return st;
         if (int rc = pmd_join(m, 10.0)) return rc;
-        if (m->per_cu <= 1) return set_err(m->c, -EIO, "pmd: workers never co-resident");
+        if (m->per_cu <= 1 || m->c->ncu * (m->per_cu - 1) < m->n_rings)
+            return set_err(m->c, -EIO, "pmd: workers never co-resident");
         m->per_cu--;
         pmd_size(m);
     }
@@ -1978,40 +2118,78 @@ static int pmd_launch_resident(cop_pmd *m, uint64_t seq0)
 
 // the kernel left: relaunch after an idle exit (every batch it completed
 // stays complete; the rest, posted before or after the exit, are served by
-// the new launch from the first incomplete one), else fail
+// the new launch from each ring's first incomplete one), else fail. Any
+// ring's thread may call it; one relaunches, the others find it running.
 static int pmd_revive(cop_pmd *m)
 {
+    if (m->h_state[0] == COPK_PMD_RUNNING) return 0;
+    std::lock_guard<std::mutex> lk(m->mu);
     const uint32_t why = m->h_state[0];
-    if (why == COPK_PMD_RUNNING) return 0;
+    if (why == COPK_PMD_RUNNING) return 0;   // another ring's thread relaunched it
     if (why != COPK_PMD_IDLE) return set_err(m->c, -EIO, "pmd kernel left (%s)", why == COPK_PMD_ABORT ?
                                              "abort: workers not co-resident, or a look-back timed out" : "stopped");
     if (int rc = pmd_join(m, 10.0)) return rc;
-    pmd_refresh(m);
-    return pmd_launch_resident(m, m->completed);
+    return pmd_launch_resident(m);
+}
+
+// ring geometry every ring of one kernel shares (the kernel is instantiated
+// once: one layout, tile size and slot count)
+static bool pmd_same_geometry(const cop_batch_ring *a, const cop_batch_ring *b)
+{
+    return a->n_slots == b->n_slots && a->n == b->n && a->stride == b->stride && a->data_off == b->data_off &&
+           (a->offsets != nullptr) == (b->offsets != nullptr) && (a->fwd_idx != nullptr) == (b->fwd_idx != nullptr) &&
+           (a->fwd_count != nullptr) == (b->fwd_count != nullptr) && a->results_slot == b->results_slot &&
+           a->fwd_slot == b->fwd_slot;
 }
 
 int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
 {
-    if (!c || !r || !out) return -EINVAL;
+    return cop_pmd_start_rings(c, r, 1, 0u, out);
+}
+
+int cop_pmd_start_rings(cop_ctx *c, const cop_batch_ring *rings, uint32_t n_rings, uint32_t flags, cop_pmd **out)
+{
+    return cop_pmd_start_rings_stages(c, rings, n_rings, flags, c ? c->cfg.stages : 0u, out);
+}
+
+int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t n_rings, uint32_t flags,
+                               uint32_t stages, cop_pmd **out)
+{
+    if (!c || !rings || !out || n_rings < 1) return -EINVAL;
     *out = nullptr;
+    if (n_rings > COPK_PMD_MAX_RINGS) return set_err(c, -EINVAL, "pmd: %u rings > %d", n_rings, COPK_PMD_MAX_RINGS);
+    if (flags & ~COP_PMD_VARIABLE_N) return set_err(c, -EINVAL, "pmd: unknown flags %#x", flags);
     if (c->pmd) return set_err(c, -EBUSY, "this context already has a poll-mode kernel");
-    if (r->n_slots == 0 || r->n == 0 || !r->pkts || !r->results) return set_err(c, -EINVAL, "pmd: empty ring");
+    const cop_batch_ring *r = &rings[0];
+    for (uint32_t q = 0; q < n_rings; q++) {
+        const cop_batch_ring *x = &rings[q];
+        if (x->n_slots == 0 || x->n == 0 || !x->pkts || !x->results) return set_err(c, -EINVAL, "pmd: empty ring");
+        if (q && !pmd_same_geometry(r, x))
+            return set_err(c, -EINVAL, "pmd: ring %u's geometry differs from ring 0's (n, slots, stride, layout)", q);
+    }
     if (r->n > c->cfg.max_batch) return set_err(c, -EINVAL, "pmd: n %u > max_batch", r->n);
     const bool imix = r->offsets != nullptr;
-    if (((uintptr_t)r->pkts & 15) || (r->pkts_slot_bytes & 15) || (r->data_off & 15) ||
-        (!imix && ((r->stride & 15) || (r->stride < 36 && r->stride != COP_HDR16_STRIDE))))
-        return set_err(c, -EINVAL, "pmd: packet starts must be 16-byte aligned");
     const bool compact = (r->fwd_idx || r->fwd_count) && !(c->cfg.flags & COP_CFG_NO_COMPACT);
     const uint32_t lists = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 1u;
-    if (r->results_slot < r->n || (r->fwd_idx && r->fwd_slot < (uint64_t)r->n * lists))
-        return set_err(c, -EINVAL, "pmd: slot sizes smaller than n (x ports with demux)");
     const bool seg = compact && (c->cfg.flags & COP_CFG_SEG_LISTS);
-    if (int rc = check_seg_ring(c, r, seg)) return rc;
+    bool wide = true;   // every slot's records 16-byte aligned (lane-pair record stores)
+    for (uint32_t q = 0; q < n_rings; q++) {
+        const cop_batch_ring *x = &rings[q];
+        if (((uintptr_t)x->pkts & 15) || (x->pkts_slot_bytes & 15) || (x->data_off & 15) ||
+            (!imix && ((x->stride & 15) || (x->stride < 36 && x->stride != COP_HDR16_STRIDE))))
+            return set_err(c, -EINVAL, "pmd: packet starts must be 16-byte aligned");
+        if (x->results_slot < x->n || (x->fwd_idx && x->fwd_slot < (uint64_t)x->n * lists))
+            return set_err(c, -EINVAL, "pmd: slot sizes smaller than n (x ports with demux)");
+        if (int rc = check_seg_ring(c, x, seg)) return rc;
+        wide = wide && ((uintptr_t)x->results & 15) == 0 && (x->results_slot & 1) == 0;
+    }
     if (int rc = sync_lanes(c)) return rc;
 
     cop_pmd *m = new (std::nothrow) cop_pmd();
     if (!m) return -ENOMEM;
     m->c = c;
+    m->n_rings = n_rings;
+    m->ring_n = r->n;
     Plan pl = plan_launch(c, (uint64_t)r->n * r->n_slots, imix, r->stride);
     // tile size: 1024-packet tiles (five workers per CU, so a 20-batch burst
     // of 64k packets is one tile per worker), 256-packet tiles for small
@@ -2026,26 +2204,32 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
     CopKParams &p = m->P.k;
     memset(&p, 0, sizeof(p));
     p.ring = 1;
-    p.rg.pkts = (const uint8_t *)r->pkts;
-    p.rg.offsets = r->offsets;
-    p.rg.results = r->results;
-    p.rg.fwd_idx = compact ? r->fwd_idx : nullptr;
-    p.rg.fwd_count = compact ? r->fwd_count : nullptr;
-    p.rg.pkts_slot_bytes = r->pkts_slot_bytes;
-    p.rg.offsets_slot_words = r->offsets_slot_words;
-    p.rg.results_slot = r->results_slot;
-    p.rg.fwd_slot = r->fwd_slot;
-    p.rg.n_slots = r->n_slots;
-    p.rg.first = 0;
-    p.rg.n = r->n;
-    p.rg.stride = r->stride;
-    p.rg.data_off = r->data_off;
+    for (uint32_t q = 0; q < n_rings; q++) {
+        const cop_batch_ring *x = &rings[q];
+        CopKRing &g = m->P.rings[q];
+        g.pkts = (const uint8_t *)x->pkts;
+        g.offsets = x->offsets;
+        g.results = x->results;
+        g.fwd_idx = compact ? x->fwd_idx : nullptr;
+        g.fwd_count = compact ? x->fwd_count : nullptr;
+        g.pkts_slot_bytes = x->pkts_slot_bytes;
+        g.offsets_slot_words = x->offsets_slot_words;
+        g.results_slot = x->results_slot;
+        g.fwd_slot = x->fwd_slot;
+        g.n_slots = x->n_slots;
+        g.first = 0;
+        g.n = x->n;
+        g.stride = x->stride;
+        g.data_off = x->data_off;
+    }
+    p.rg = m->P.rings[0];
+    m->P.n_rings = n_rings;
     p.nb = 1;
     p.ntiles = m->tpb;
     p.uniform_ntiles = m->tpb;
     p.compact = compact ? 1u : 0u;
     p.seg = seg ? 1u : 0u;
-    p.stages = c->cfg.stages;
+    p.stages = stages;
     p.demux = (compact && (c->cfg.flags & COP_CFG_DEMUX_PORTS)) ? c->cfg.n_ports : 0u;
     int rc = 0;
 #define PMD_FAIL(code)       \
@@ -2054,13 +2238,12 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         goto fail;           \
     } while (0)
     {
-        // records as 16-byte write-through stores from LDS: every slot's
-        // records 16-byte aligned
+        // records as 16-byte write-through stores: every slot's records
+        // 16-byte aligned
         // ($COP_PMD_REC: paired = from lane pairs in registers, the default;
         // stage = through an LDS stage after the compaction; 8 = 8-byte stores)
         const char *rec_env = getenv("COP_PMD_REC");
-        const bool wide = ((uintptr_t)r->results & 15) == 0 && (r->results_slot & 1) == 0 &&
-                          !(rec_env && !strcmp(rec_env, "8"));
+        wide = wide && !(rec_env && !strcmp(rec_env, "8"));
         const bool stage_rec = wide && rec_env && !strcmp(rec_env, "stage");
         if ((rc = fill_launch(c, p, ppt, &m->fw_mode, &m->lpm_mode, &m->lds_bytes, stage_rec))) goto fail;
         p.rec_paired = wide && !stage_rec ? 1u : 0u;
@@ -2076,7 +2259,8 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         }
         // per-rule hits by binning, as in the one-shot kernel: one region per
         // (slot, tile), counted by cop_hit_count beside the running kernel
-        if (p.rule_hits && c->hit_bins) {
+        // (one ring; with several, one atomic per hit)
+        if (p.rule_hits && c->hit_bins && n_rings == 1) {
             const uint32_t nb = (c->n_rule_ctr + (1u << COPK_HIT_SHIFT) - 1) >> COPK_HIT_SHIFT;
             const uint32_t reg = COPK_BLOCK * (uint32_t)ppt + 4u * nb;
             const uint32_t base = (m->lds_bytes / 4u + 3u) & ~3u;
@@ -2117,32 +2301,37 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
             const unsigned long long ms = std::min<unsigned long long>(strtoull(env, nullptr, 0), 86400000ull);
             m->P.idle_ticks = std::max<unsigned long long>(ms, 1ull) * 100000ull;
         }
-        // control block in mapped host memory: posted, stop, state, then one
-        // completion word per slot
-        const size_t ctl_bytes = 64 + (size_t)m->n_slots * 8;
+        // control block in mapped host memory: posted words, stop, state,
+        // then the completion words (and the batch sizes) of every ring slot
+        const size_t words = (size_t)n_rings * m->n_slots;
+        const bool var_n = (flags & COP_PMD_VARIABLE_N) != 0;
+        const size_t ctl_bytes = PMD_H_DONE + words * 8 + (var_n ? words * 4 : 0);
         HIPCHK(c, hipSetDevice(c->device));
         if (hipHostMalloc(&m->ctl, ctl_bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             PMD_FAIL(set_err(c, -ENOMEM, "pmd: host control block"));
         memset(m->ctl, 0, ctl_bytes);
         void *dctl = nullptr;
         if (hipHostGetDevicePointer(&dctl, m->ctl, 0) != hipSuccess) PMD_FAIL(set_err(c, -EIO, "pmd: mapping"));
-        m->h_posted = (volatile uint64_t *)m->ctl;
-        m->h_stop = (volatile uint32_t *)(m->ctl + 8);
-        m->h_state = (volatile uint32_t *)(m->ctl + 16);
-        m->h_done = (volatile uint64_t *)(m->ctl + 64);
+        m->h_stop = (volatile uint32_t *)(m->ctl + PMD_H_STOP);
+        m->h_state = (volatile uint32_t *)(m->ctl + PMD_H_STATE);
+        m->h_done = (volatile uint64_t *)(m->ctl + PMD_H_DONE);
         m->P.h_posted = (const unsigned long long *)dctl;
-        m->P.h_stop = (const uint32_t *)((uint8_t *)dctl + 8);
-        m->P.h_state = (uint32_t *)((uint8_t *)dctl + 16);
-        m->P.h_done = (unsigned long long *)((uint8_t *)dctl + 64);
-        // device words: control and relays, slot tile counts, then the
+        m->P.h_stop = (const uint32_t *)((uint8_t *)dctl + PMD_H_STOP);
+        m->P.h_state = (uint32_t *)((uint8_t *)dctl + PMD_H_STATE);
+        m->P.h_done = (unsigned long long *)((uint8_t *)dctl + PMD_H_DONE);
+        if (var_n) {
+            m->h_n = (volatile uint32_t *)(m->ctl + PMD_H_DONE + words * 8);
+            m->P.h_n = (const uint32_t *)((uint8_t *)dctl + PMD_H_DONE + words * 8);
+        }
+        // device words: control, gates and relays, slot tile counts, then the
         // look-back chains (dense lists only)
         // one slot counter per 4160 bytes: 64 returning adds per batch on
         // counters packed 16 to a line held a 20-batch burst up ~3 us
         // (tools/burst modes 15/16, profiles/r03/burst/burst7)
         m->P.slot_stride = 520;
         if (const char *e = getenv("COP_PMD_SLOT_STRIDE")) m->P.slot_stride = std::max(1u, (uint32_t)atoi(e));
-        const size_t look_off = (PMD_CTL_BYTES + (size_t)m->n_slots * m->P.slot_stride * 8 + 255) & ~(size_t)255;
-        const size_t look_words = (compact && !seg) ? (size_t)m->n_slots * m->tpb * (p.demux ? p.demux : 1u) : 0;
+        const size_t look_off = (PMD_CTL_BYTES + words * m->P.slot_stride * 8 + 255) & ~(size_t)255;
+        const size_t look_words = (compact && !seg) ? words * m->tpb * (p.demux ? p.demux : 1u) : 0;
         m->dev_bytes = look_off + look_words * 8;
         if (getenv("COP_PMD_STAMPS")) {   // diagnostic phase stamps (cop_debug_pmd_stamps)
             if (hipMalloc(&m->P.stamps, ((size_t)m->P.n_work * 8 + 128) * 8) != hipSuccess)
@@ -2153,13 +2342,16 @@ int cop_pmd_start(cop_ctx *c, const cop_batch_ring *r, cop_pmd **out)
         if (hipMalloc(&m->dev, m->dev_bytes) != hipSuccess) PMD_FAIL(set_err(c, -ENOMEM, "pmd: device words"));
         if (hipStreamCreateWithFlags(&m->s, hipStreamNonBlocking) != hipSuccess)
             PMD_FAIL(set_err(c, -EIO, "pmd: stream"));
-        m->P.d_posted = (unsigned long long *)(m->dev + PMD_RELAY_OFF);
         m->P.d_ctl = (uint32_t *)(m->dev + 8);
+        m->P.d_act = (unsigned long long *)(m->dev + PMD_ACT_OFF);
+        m->P.d_gate = (unsigned long long *)(m->dev + PMD_GATE_OFF);
+        m->P.d_posted = (unsigned long long *)(m->dev + PMD_RELAY_OFF);
         m->P.slot_tiles = (unsigned long long *)(m->dev + PMD_CTL_BYTES);
         p.look = look_words ? (unsigned long long *)(m->dev + look_off) : nullptr;
         p.err = nullptr;   // the look-back reports through d_ctl[2] (LookCtx)
         p.epoch = 0;
-        if ((rc = pmd_launch_resident(m, 0))) {
+        if ((rc = pmd_prewarm(m))) goto fail;
+        if ((rc = pmd_launch_resident(m))) {
             (void)pmd_join(m, 10.0);
             goto fail;
         }
@@ -2181,49 +2373,84 @@ fail:
     return rc;
 }
 
-int cop_pmd_post(cop_pmd *m, uint32_t count)
+int cop_pmd_wait_ring(cop_pmd *m, uint32_t ring, uint64_t seq)
 {
-    if (!m) return -EINVAL;
-    if (count == 0) return 0;
-    if (count > m->n_slots) return set_err(m->c, -EINVAL, "pmd: post of %u > %u ring slots", count, m->n_slots);
-    // a slot is reposted only after its previous batch completed
-    const uint64_t need = m->posted + count;
-    if (need - m->completed > m->n_slots)
-        if (int rc = cop_pmd_wait(m, need - m->n_slots)) return rc;
-    if (need > m->n_slots)   // the reused slots' binned hits are counted first
-        if (int rc = pmd_hits_sync(m, need - m->n_slots)) return rc;
-    if (int rc = pmd_revive(m)) return rc;
-    std::atomic_thread_fence(std::memory_order_seq_cst);   // ring slots written before the doorbell
-    *m->h_posted = need;
-    m->posted = need;
-    return 0;
-}
-
-int cop_pmd_wait(cop_pmd *m, uint64_t seq)
-{
-    if (!m) return -EINVAL;
-    if (seq > m->posted) return set_err(m->c, -EINVAL, "pmd: wait for %llu > %llu posted", (unsigned long long)seq,
-                                        (unsigned long long)m->posted);
+    if (!m || ring >= m->n_rings) return -EINVAL;
+    PmdRing &g = m->ring[ring];
+    const uint64_t posted = g.posted.load(std::memory_order_relaxed);
+    if (seq > posted)
+        return set_err(m->c, -EINVAL, "pmd: ring %u: wait for %llu > %llu posted", ring, (unsigned long long)seq,
+                       (unsigned long long)posted);
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t spins = 0;
     for (;;) {
-        pmd_refresh(m);
-        if (m->completed >= seq) break;
+        if (pmd_refresh(m, ring) >= seq) break;
         if (m->h_state[0] != COPK_PMD_RUNNING) {
-            pmd_refresh(m);   // its last completion may have landed just before it left
-            if (m->completed >= seq) break;
+            if (pmd_refresh(m, ring) >= seq) break;   // its last completion may have landed just before it left
             if (int rc = pmd_revive(m)) return rc;
         }
         if ((++spins & 1023u) == 0 &&
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 30.0)
-            return set_err(m->c, -ETIMEDOUT, "pmd: batch %llu not complete after 30 s",
-                           (unsigned long long)m->completed);
+            return set_err(m->c, -ETIMEDOUT, "pmd: ring %u: batch %llu not complete after 30 s", ring,
+                           (unsigned long long)g.completed.load());
     }
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    return pmd_hits_launch(m);
+    return ring == 0 ? pmd_hits_launch(m) : 0;
 }
 
-uint64_t cop_pmd_posted(const cop_pmd *m) { return m ? m->posted : 0; }
+int cop_pmd_wait(cop_pmd *m, uint64_t seq) { return cop_pmd_wait_ring(m, 0, seq); }
+
+// Post `count` batches to ring r; n_each: their packets (variable-n rings),
+// 0 = the ring's n
+static int pmd_post(cop_pmd *m, uint32_t r, uint32_t count, uint32_t n_each)
+{
+    if (count == 0) return 0;
+    if (count > m->n_slots) return set_err(m->c, -EINVAL, "pmd: post of %u > %u ring slots", count, m->n_slots);
+    PmdRing &g = m->ring[r];
+    const uint64_t posted = g.posted.load(std::memory_order_relaxed);
+    // a slot is reposted only after its previous batch completed
+    const uint64_t need = posted + count;
+    if (need - g.completed.load(std::memory_order_relaxed) > m->n_slots)
+        if (int rc = cop_pmd_wait_ring(m, r, need - m->n_slots)) return rc;
+    if (r == 0 && need > m->n_slots)   // the reused slots' binned hits are counted first
+        if (int rc = pmd_hits_sync(m, need - m->n_slots)) return rc;
+    if (int rc = pmd_revive(m)) return rc;
+    if (m->h_n)
+        for (uint64_t b = posted; b < need; b++)
+            m->h_n[(size_t)r * m->n_slots + b % m->n_slots] = n_each ? n_each : m->ring_n;
+    std::atomic_thread_fence(std::memory_order_seq_cst);   // ring slots (and sizes) written before the doorbell
+    *m->h_posted(r) = need;
+    g.posted.store(need, std::memory_order_relaxed);
+    return 0;
+}
+
+int cop_pmd_post_ring(cop_pmd *m, uint32_t ring, uint32_t count)
+{
+    if (!m || ring >= m->n_rings) return -EINVAL;
+    return pmd_post(m, ring, count, 0);
+}
+
+int cop_pmd_post(cop_pmd *m, uint32_t count) { return cop_pmd_post_ring(m, 0, count); }
+
+int cop_pmd_post_batch(cop_pmd *m, uint32_t ring, uint32_t n)
+{
+    if (!m || ring >= m->n_rings) return -EINVAL;
+    if (!m->h_n) return set_err(m->c, -EINVAL, "pmd: started without COP_PMD_VARIABLE_N");
+    if (n == 0 || n > m->ring_n) return set_err(m->c, -EINVAL, "pmd: batch of %u packets (1..%u)", n, m->ring_n);
+    return pmd_post(m, ring, 1, n);
+}
+
+uint64_t cop_pmd_posted(const cop_pmd *m) { return m ? m->ring[0].posted.load() : 0; }
+
+uint64_t cop_pmd_posted_ring(const cop_pmd *m, uint32_t ring)
+{
+    return m && ring < m->n_rings ? m->ring[ring].posted.load() : 0;
+}
+
+uint64_t cop_pmd_completed_ring(cop_pmd *m, uint32_t ring)
+{
+    return m && ring < m->n_rings ? pmd_refresh(m, ring) : 0;
+}
 
 int cop_pmd_run(cop_pmd *m, uint64_t count)
 {
@@ -2234,7 +2461,7 @@ int cop_pmd_run(cop_pmd *m, uint64_t count)
         if (int rc = cop_pmd_post(m, k)) return rc;
         done += k;
     }
-    return cop_pmd_wait(m, m->posted);
+    return cop_pmd_wait(m, m->ring[0].posted.load());
 }
 
 int cop_pmd_info(const cop_pmd *m, cop_pmd_info_t *out)
@@ -2244,10 +2471,13 @@ int cop_pmd_info(const cop_pmd *m, cop_pmd_info_t *out)
     out->workers_per_cu = m->per_cu;
     out->tiles_per_batch = m->tpb;
     out->packets_per_tile = COPK_BLOCK * (uint32_t)m->ppt;
-    out->launches = m->launches;
+    out->launches = m->launches.load();
     out->state = m->h_state[0];
-    out->posted = m->posted;
-    out->completed = m->completed;
+    out->posted = out->completed = 0;
+    for (uint32_t r = 0; r < m->n_rings; r++) {   // every ring's batches
+        out->posted += m->ring[r].posted.load();
+        out->completed += m->ring[r].completed.load();
+    }
     return 0;
 }
 
@@ -2255,8 +2485,9 @@ int cop_pmd_stop(cop_pmd *m)
 {
     if (!m) return -EINVAL;
     cop_ctx *c = m->c;
-    int rc = cop_pmd_wait(m, m->posted);
-    if (!rc) rc = pmd_hits_sync(m, m->completed);
+    int rc = 0;
+    for (uint32_t r = 0; r < m->n_rings && !rc; r++) rc = cop_pmd_wait_ring(m, r, m->ring[r].posted.load());
+    if (!rc) rc = pmd_hits_sync(m, m->ring[0].completed.load());
     *m->h_stop = 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     const int jrc = pmd_join(m, 10.0);
@@ -2312,6 +2543,14 @@ int cop_debug_stamps(cop_ctx *c, uint64_t *out, uint32_t max_words)
     if (int rc = sync_lanes(c)) return rc;
     HIPCHK(c, hipMemcpy(out, c->stamps, (size_t)n * 8, hipMemcpyDeviceToHost));
     return (int)n;
+}
+
+int cop_debug_host_prof(cop_ctx *c, uint64_t *out, uint32_t n, int reset)
+{
+    if (!c || !out) return -EINVAL;
+    for (uint32_t i = 0; i < n && i < 6; i++) out[i] = c->hp[i];
+    if (reset) memset(c->hp, 0, sizeof(c->hp));
+    return 6;
 }
 
 int cop_launch_timing(cop_ctx *c, int enable)

@@ -307,9 +307,10 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
 // WT: write-through output stores (poll-mode). sync_tables: wait for the
 // LDS-DMA table staging after the header loads are issued. hit_tile: the
 // tile's binned-hit region index (one-shot: blockIdx; poll mode: its slot's
-// tile).
+// tile). Returns false when the tile's look-back gave up (poll-mode abort):
+// the tile must not be counted as done (workgroup-uniform).
 template <int FW, int LPM, int LAY, int PPT, bool EXT, bool WT>
-__device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, const LdsCarve &lc, const CopKBatch &B,
+__device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, const LdsCarve &lc, const CopKBatch &B,
                                           uint32_t look_off, uint32_t j, const LookCtx &lk, int tid, int lane, int wave,
                                           bool sync_tables, size_t hit_tile)
 {
@@ -411,7 +412,7 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
         seg_epilogue<FW, PPT, WT>(p, B, base, valid, verdict, flags, lc.cl, lc.s_red, tid, lane, wave, records);
         STAMP(5);
         STAMP(6);
-        return;
+        return true;
     }
     if (bins) hit_hist<PPT>(hit_lds<PPT>(p, lc.s_misc - p.lds_misc_off), valid, flags, fwe, tid, p.hit_nb == 1);
     else rule_hit_atomics<FW, PPT>(o, valid, flags, fwe);
@@ -433,8 +434,9 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
         if (paired) store_records_paired<PPT, WT>(B, base, tid, lane, wave, valid, verdict, flags, port, rnh, fwd, cn);
         else store_records<PPT, WT>(B, base, tid, valid, verdict, flags, port, rnh, fwd, cn, rec_stage);
     };
+    bool ok = true;
     if (p.compact)
-        compact_tile<PPT, WT>(lk, o, B, look_off, j, base, fwd, port, p.seg != 0, lc.cl, tid, lane, wave, records);
+        ok = compact_tile<PPT, WT>(lk, o, B, look_off, j, base, fwd, port, p.seg != 0, lc.cl, tid, lane, wave, records);
     else records();
     if (rec_stage) {
         // compact_tile's second barrier (or this one) orders the staged records
@@ -442,6 +444,7 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
         copy_out_records<WT>(B.results, base, B.n > base ? min(B.n - base, (uint32_t)TILE) : 0u, rec_stage, tid);
     }
     STAMP(5);
+    if (!ok) return false;   // gave up (abort): no counters, no hit region
 
     // ---- counters (one flush per workgroup) ----
     uint32_t prx[COPK_MAX_DEMUX_PORTS] = {}, ptx[COPK_MAX_DEMUX_PORTS] = {};
@@ -450,6 +453,7 @@ __device__ __forceinline__ void tile_body(const CopKParams &p, const Opt &o, con
     // (flush_counters' barrier has landed every hit_hist add)
     if (bins) hit_sort_out<PPT, WT>(p, hit_lds<PPT>(p, lc.s_misc - p.lds_misc_off), tid, lane, wave, hit_tile);
     STAMP(6);
+    return true;
 }
 
 }  // namespace copd

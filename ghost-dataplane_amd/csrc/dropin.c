@@ -19,11 +19,13 @@
  * process globals (firewall.h:107-110). Here every calling thread gets its
  * own context in thread-local storage, so the threads share nothing.
  */
+#define _POSIX_C_SOURCE 199309L   /* clock_gettime (diagnostic profile) */
 #include <errno.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #define COP_NO_DROPIN_MACROS 1   /* this file defines the functions the macros call */
 #include "cop_gpu.h"
@@ -55,6 +57,39 @@ static __thread struct {
     cop_result *res;
     uint32_t cap;
 } tl_buf;
+
+/* Diagnostic per-op host time of this thread's ring loop ($COP_HOST_PROF=1,
+ * cop_debug_dropin_prof): ns in drain (dequeue + mbuf data addresses),
+ * batch (cop_process_host_stages: gather, launch, wait, copy-out; or the
+ * async submit: gather + launch), wait (async completion), forward (tx
+ * enqueue + frees); then calls, calls that found packets, packets. */
+enum { PROF_DRAIN, PROF_BATCH, PROF_WAIT, PROF_FWD, PROF_CALLS, PROF_BUSY_CALLS, PROF_PKTS, PROF_N };
+static __thread uint64_t tl_prof[PROF_N];
+static int g_prof = -1;
+
+static inline int prof_on(void)
+{
+    if (g_prof < 0) {
+        const char *e = getenv("COP_HOST_PROF");
+        g_prof = e && atoi(e) ? 1 : 0;
+    }
+    return g_prof;
+}
+
+static inline uint64_t prof_ns(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+int cop_debug_dropin_prof(uint64_t *out, uint32_t n, int reset)
+{
+    if (!out) return -EINVAL;
+    for (uint32_t i = 0; i < n && i < PROF_N; i++) out[i] = tl_prof[i];
+    if (reset) memset(tl_prof, 0, sizeof(tl_prof));
+    return PROF_N;
+}
 
 void cop_set_mbuf_layout(uint32_t buf_addr_off, uint32_t data_off_off)
 {
@@ -96,6 +131,16 @@ int cop_coprocessor_setup_stages(uint32_t stages)
     int rc = cop_set_dropin_stages(stages);
     if (rc) return 1;
     return coprocessor_setup();
+}
+
+int cop_coprocessor_setup_fw(void)
+{
+    return cop_coprocessor_setup_stages(COP_STAGE_FW);
+}
+
+int cop_coprocessor_setup_no_nf(void)
+{
+    return cop_coprocessor_setup_stages(0u);
 }
 
 cop_ctx *coprocessor_ctx(void)
@@ -277,14 +322,32 @@ int cop_coprocessor_poll(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_t max_
      * would strand every mbuf it dequeued */
     if (max_pkts > cop_ctx_max_batch(ctx)) return -EINVAL;
     if (ensure_buf(max_pkts)) return -ENOMEM;
+    const int prof = prof_on();
+    uint64_t t0 = prof ? prof_ns() : 0;
     const uint32_t n = drain_rx(rx, tl_buf.objs, tl_buf.data, max_pkts);
+    if (prof) {
+        const uint64_t t1 = prof_ns();
+        tl_prof[PROF_DRAIN] += t1 - t0;
+        tl_prof[PROF_CALLS]++;
+        t0 = t1;
+    }
     if (n == 0) return 0;
     int rc = cop_process_host_stages(ctx, g_dropin_stages, tl_buf.data, n, tl_buf.res, NULL, NULL);
     if (rc) {
         drop_all(tl_buf.objs, n, free_fn, free_arg, stats);
         return rc;
     }
+    if (prof) {
+        const uint64_t t1 = prof_ns();
+        tl_prof[PROF_BATCH] += t1 - t0;
+        t0 = t1;
+    }
     forward_batch(tx, tl_buf.objs, tl_buf.res, n, free_fn, free_arg, stats);
+    if (prof) {
+        tl_prof[PROF_FWD] += prof_ns() - t0;
+        tl_prof[PROF_BUSY_CALLS]++;
+        tl_prof[PROF_PKTS] += n;
+    }
     return (int)n;
 }
 
@@ -294,7 +357,14 @@ static int async_complete_oldest(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn
     const uint32_t s = tl_async.fifo[0];
     const cop_result *res = NULL;
     uint32_t n = 0;
+    const int prof = prof_on();
+    uint64_t t0 = prof ? prof_ns() : 0;
     int rc = cop_host_batch_wait(ctx, s, &res, &n);
+    if (prof) {
+        const uint64_t t1 = prof_ns();
+        tl_prof[PROF_WAIT] += t1 - t0;
+        t0 = t1;
+    }
     for (uint32_t i = 1; i < tl_async.depth; i++) tl_async.fifo[i - 1] = tl_async.fifo[i];
     tl_async.depth--;
     if (rc) {
@@ -305,6 +375,10 @@ static int async_complete_oldest(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn
     }
     forward_batch(tx, tl_async.objs[s], res, n, free_fn, free_arg, stats);
     tl_async.n[s] = 0;
+    if (prof) {
+        tl_prof[PROF_FWD] += prof_ns() - t0;
+        tl_prof[PROF_PKTS] += n;
+    }
     return (int)n;
 }
 
@@ -340,13 +414,23 @@ int cop_coprocessor_poll_async(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_
         tl_async.data = d;
         tl_async.data_cap = max_pkts;
     }
+    const int prof = prof_on();
+    uint64_t t0 = prof ? prof_ns() : 0;
     const uint32_t n = drain_rx(rx, tl_async.objs[s], tl_async.data, max_pkts);
+    if (prof) {
+        const uint64_t t1 = prof_ns();
+        tl_prof[PROF_DRAIN] += t1 - t0;
+        tl_prof[PROF_CALLS]++;
+        tl_prof[PROF_BUSY_CALLS] += n != 0;
+        t0 = t1;
+    }
     if (n) {
         int rc = cop_host_batch_submit_stages(ctx, g_dropin_stages, s, tl_async.data, n);
         if (rc) {
             drop_all(tl_async.objs[s], n, free_fn, free_arg, stats);
             return rc;
         }
+        if (prof) tl_prof[PROF_BATCH] += prof_ns() - t0;
         tl_async.n[s] = n;
         tl_async.ctx = ctx;
         tl_async.fifo[tl_async.depth++] = s;
@@ -373,6 +457,178 @@ int cop_coprocessor_flush(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn, void 
             continue;
         }
         done += r;
+    }
+    return err ? err : done;
+}
+
+/* ---- the drop-in ring loop on one shared poll-mode kernel ---------------
+ * The reference runs one coprocessor lcore per vport, each polling its own
+ * rx ring (main.c:92-94, switch.c:463). Here ONE poll-mode kernel serves
+ * every such thread's ring: ring r's batches are the 16-byte header records
+ * of one drain of rx ring r, gathered into mapped pinned host memory (the
+ * kernel reads them over PCIe and writes its records back there), posted
+ * with their packet count; no launch per batch. */
+struct cop_pmd_host {
+    cop_ctx *ctx;
+    cop_pmd *pmd;
+    uint32_t n_rings, n_slots, max_pkts;
+    uint8_t *h_stage;         /* [ring][slot][max_pkts] 16-byte header records (mapped) */
+    cop_result *h_res;        /* [ring][slot][max_pkts] result records (mapped) */
+    struct {
+        void **objs;          /* [slot][max_pkts] the mbufs each slot in flight holds */
+        const void **data;    /* [max_pkts] the data addresses of one drain */
+        uint32_t *n;          /* [slot] mbufs held */
+        uint64_t head;        /* the ring's oldest batch in flight (its sequence number) */
+    } ring[COP_PMD_MAX_RINGS];
+};
+
+int cop_pmd_host_destroy(cop_pmd_host *h)
+{
+    if (!h) return -EINVAL;
+    int rc = h->pmd ? cop_pmd_stop(h->pmd) : 0;
+    if (h->h_stage) cop_host_free_pinned(h->ctx, h->h_stage);
+    if (h->h_res) cop_host_free_pinned(h->ctx, h->h_res);
+    for (uint32_t r = 0; r < COP_PMD_MAX_RINGS; r++) {
+        free(h->ring[r].objs);
+        free((void *)h->ring[r].data);
+        free(h->ring[r].n);
+    }
+    free(h);
+    return rc;
+}
+
+int cop_pmd_host_create(cop_ctx *ctx, uint32_t n_rings, uint32_t max_pkts, uint32_t n_slots, cop_pmd_host **out)
+{
+    if (!ctx || !out || n_rings < 1 || n_rings > COP_PMD_MAX_RINGS || max_pkts < 1 || n_slots < 1) return -EINVAL;
+    if (max_pkts > cop_ctx_max_batch(ctx)) return -EINVAL;
+    *out = NULL;
+    cop_pmd_host *h = (cop_pmd_host *)calloc(1, sizeof(*h));
+    if (!h) return -ENOMEM;
+    h->ctx = ctx;
+    h->n_rings = n_rings;
+    h->n_slots = n_slots;
+    h->max_pkts = max_pkts = (max_pkts + 1u) & ~1u;   /* even: 16-byte aligned record slots */
+    const size_t recs = (size_t)n_rings * n_slots * max_pkts;
+    void *d_stage = NULL, *d_res = NULL;
+    int rc = cop_host_alloc_mapped(ctx, recs * COP_HDR16_STRIDE, (void **)&h->h_stage, &d_stage);
+    if (!rc) rc = cop_host_alloc_mapped(ctx, recs * sizeof(cop_result), (void **)&h->h_res, &d_res);
+    cop_batch_ring rings[COP_PMD_MAX_RINGS];
+    for (uint32_t r = 0; !rc && r < n_rings; r++) {
+        h->ring[r].objs = (void **)calloc((size_t)n_slots * max_pkts, sizeof(void *));
+        h->ring[r].data = (const void **)calloc(max_pkts, sizeof(void *));
+        h->ring[r].n = (uint32_t *)calloc(n_slots, sizeof(uint32_t));
+        if (!h->ring[r].objs || !h->ring[r].data || !h->ring[r].n) rc = -ENOMEM;
+        memset(&rings[r], 0, sizeof(rings[r]));
+        rings[r].pkts = (uint8_t *)d_stage + (size_t)r * n_slots * max_pkts * COP_HDR16_STRIDE;
+        rings[r].n_slots = n_slots;
+        rings[r].n = max_pkts;
+        rings[r].stride = COP_HDR16_STRIDE;
+        rings[r].pkts_slot_bytes = (uint64_t)max_pkts * COP_HDR16_STRIDE;
+        rings[r].results = (cop_result *)d_res + (size_t)r * n_slots * max_pkts;
+        rings[r].results_slot = max_pkts;
+    }
+    if (!rc) rc = cop_pmd_start_rings_stages(ctx, rings, n_rings, COP_PMD_VARIABLE_N, g_dropin_stages, &h->pmd);
+    if (rc) {
+        cop_pmd_host_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return 0;
+}
+
+/* complete ring r's oldest batch in flight: forward / free its mbufs */
+static int pmd_host_complete(cop_pmd_host *h, uint32_t r, cop_ring *tx, cop_free_fn free_fn, void *free_arg,
+                             cop_nf_stats *stats)
+{
+    const uint64_t b = h->ring[r].head;
+    const uint32_t slot = (uint32_t)(b % h->n_slots);
+    void **objs = h->ring[r].objs + (size_t)slot * h->max_pkts;
+    const uint32_t n = h->ring[r].n[slot];
+    const int prof = prof_on();
+    uint64_t t0 = prof ? prof_ns() : 0;
+    int rc = cop_pmd_wait_ring(h->pmd, r, b + 1);
+    if (prof) {
+        const uint64_t t1 = prof_ns();
+        tl_prof[PROF_WAIT] += t1 - t0;
+        t0 = t1;
+    }
+    h->ring[r].head = b + 1;
+    h->ring[r].n[slot] = 0;
+    if (rc) {
+        drop_all(objs, n, free_fn, free_arg, stats);   /* no verdicts: freed, never leaked */
+        return rc;
+    }
+    const cop_result *res = h->h_res + ((size_t)r * h->n_slots + slot) * h->max_pkts;
+    forward_batch(tx, objs, res, n, free_fn, free_arg, stats);
+    if (prof) {
+        tl_prof[PROF_FWD] += prof_ns() - t0;
+        tl_prof[PROF_PKTS] += n;
+    }
+    return (int)n;
+}
+
+int cop_coprocessor_poll_pmd(cop_pmd_host *h, uint32_t r, cop_ring *rx, cop_ring *tx, uint32_t max_pkts,
+                             cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats)
+{
+    if (!h || r >= h->n_rings || !rx || !tx) return -EINVAL;
+    if (max_pkts == 0) max_pkts = COP_PKT_BURST_SZ;
+    if (max_pkts > h->max_pkts) return -EINVAL;   /* before any dequeue */
+    int done = 0;
+    uint64_t posted = cop_pmd_posted_ring(h->pmd, r);
+    /* a free slot: complete the oldest batch if every slot is in flight */
+    if (posted - h->ring[r].head == h->n_slots) {
+        int c = pmd_host_complete(h, r, tx, free_fn, free_arg, stats);
+        if (c < 0) return c;
+        done += c;
+    }
+    const uint32_t slot = (uint32_t)(posted % h->n_slots);
+    void **objs = h->ring[r].objs + (size_t)slot * h->max_pkts;
+    const int prof = prof_on();
+    uint64_t t0 = prof ? prof_ns() : 0;
+    const uint32_t n = drain_rx(rx, objs, h->ring[r].data, max_pkts);
+    if (prof) {
+        const uint64_t t1 = prof_ns();
+        tl_prof[PROF_DRAIN] += t1 - t0;
+        tl_prof[PROF_CALLS]++;
+        tl_prof[PROF_BUSY_CALLS] += n != 0;
+        t0 = t1;
+    }
+    if (n) {
+        cop_pack_headers(h->ring[r].data, n,
+                         h->h_stage + (((size_t)r * h->n_slots + slot) * h->max_pkts) * COP_HDR16_STRIDE);
+        int rc = cop_pmd_post_batch(h->pmd, r, n);
+        if (rc) {
+            drop_all(objs, n, free_fn, free_arg, stats);
+            return rc;
+        }
+        h->ring[r].n[slot] = n;
+        posted++;
+        if (prof) tl_prof[PROF_BATCH] += prof_ns() - t0;
+    }
+    /* complete, oldest first, every batch already done; with rx empty, the
+     * oldest in flight too (waiting for it) */
+    while (posted > h->ring[r].head) {
+        if (cop_pmd_completed_ring(h->pmd, r) <= h->ring[r].head && n != 0) break;
+        int c = pmd_host_complete(h, r, tx, free_fn, free_arg, stats);
+        if (c < 0) return c;
+        done += c;
+        if (n == 0) break;
+    }
+    return done;
+}
+
+int cop_coprocessor_flush_pmd(cop_pmd_host *h, uint32_t r, cop_ring *tx, cop_free_fn free_fn, void *free_arg,
+                              cop_nf_stats *stats)
+{
+    if (!h || r >= h->n_rings || !tx) return -EINVAL;
+    int done = 0, err = 0;
+    while (cop_pmd_posted_ring(h->pmd, r) > h->ring[r].head) {
+        int c = pmd_host_complete(h, r, tx, free_fn, free_arg, stats);
+        if (c < 0) {
+            if (!err) err = c;   /* keep completing: every held mbuf is forwarded or freed */
+            continue;
+        }
+        done += c;
     }
     return err ? err : done;
 }

@@ -409,11 +409,36 @@ typedef struct cop_pmd_info_t {
     uint32_t packets_per_tile;
     uint32_t launches;         /* 1 + relaunches after idle exits */
     uint32_t state;            /* 0 running, 1 stopped, 2 left idle, 3 aborted */
-    uint64_t posted, completed;
+    uint64_t posted, completed; /* summed over the rings */
 } cop_pmd_info_t;
 int cop_pmd_info(const cop_pmd *pmd, cop_pmd_info_t *out);
 /* Complete everything posted, stop the kernel, free. */
 int cop_pmd_stop(cop_pmd *pmd);
+
+/* Several rx rings served by ONE poll-mode kernel: the GPU form of the
+ * reference's five coprocessor lcores, each polling its own rx ring
+ * (KNI_KTHREAD, main.c:92-94, switch.c:463). The kernel's workers are split
+ * among the rings (worker w serves ring w % n_rings); each ring has its own
+ * batch sequence, doorbell and completion words, so its batches complete in
+ * its own order and one ring's thread never waits for another's. Every ring
+ * must have ring 0's geometry (n, n_slots, stride, data_off, layout, slot
+ * sizes); the pointers are each ring's own. Ring r is posted and waited by
+ * one thread (different rings from different threads). At most
+ * COP_PMD_MAX_RINGS. The single-ring calls above act on ring 0. */
+#define COP_PMD_MAX_RINGS 8
+#define COP_PMD_VARIABLE_N 1u   /* batches carry their own packet count (cop_pmd_post_batch) */
+int cop_pmd_start_rings(cop_ctx *ctx, const cop_batch_ring *rings, uint32_t n_rings, uint32_t flags,
+                        cop_pmd **out);
+/* Post the next `count` full batches (n packets each) of one ring. */
+int cop_pmd_post_ring(cop_pmd *pmd, uint32_t ring, uint32_t count);
+/* Post ONE batch of n (1..ring n) packets to one ring: the packets
+ * 0..n-1 of its next slot (COP_PMD_VARIABLE_N). */
+int cop_pmd_post_batch(cop_pmd *pmd, uint32_t ring, uint32_t n);
+/* As cop_pmd_wait, for one ring's sequence numbers. */
+int cop_pmd_wait_ring(cop_pmd *pmd, uint32_t ring, uint64_t seq);
+uint64_t cop_pmd_posted_ring(const cop_pmd *pmd, uint32_t ring);
+/* Batches of the ring known complete (reads the completion words). */
+uint64_t cop_pmd_completed_ring(cop_pmd *pmd, uint32_t ring);
 
 /* Counters (u64, device-resident, summed over every submitted packet).
  * On the device they are kept in COP_COUNTER_SHARDS shards of
@@ -548,9 +573,20 @@ int cop_set_dropin_stages(uint32_t stages);
 uint32_t cop_dropin_stages(void);
 /* cop_set_dropin_stages(stages), then coprocessor_setup(). */
 int cop_coprocessor_setup_stages(uint32_t stages);
+/* coprocessor_setup() with a fixed chain: the firewall (ENABLE_FW_NF), or
+ * none (DISABLE_NF). Same signature as coprocessor_setup. */
+int cop_coprocessor_setup_fw(void);
+int cop_coprocessor_setup_no_nf(void);
 #ifndef COP_NO_DROPIN_MACROS
-/* the caller's ENABLE_FW_NF / DISABLE_NF select the chain (see COP_DROPIN_STAGES) */
-#define coprocessor_setup() cop_coprocessor_setup_stages(COP_DROPIN_STAGES)
+/* The caller's ENABLE_FW_NF / DISABLE_NF select the chain (see
+ * COP_DROPIN_STAGES). An object-like alias: the reference's own declaration
+ * `int coprocessor_setup(void);` (coprocessor.h:30) after this header still
+ * compiles, and &coprocessor_setup is a function pointer. */
+#if defined(DISABLE_NF) || defined(COP_DROPIN_NO_NF)
+#define coprocessor_setup cop_coprocessor_setup_no_nf
+#else
+#define coprocessor_setup cop_coprocessor_setup_fw
+#endif
 #endif
 int coprocessor_teardown(void);
 /* 0 = forward, -1 = drop (coprocessor.c:50-65). One-packet GPU batch:
@@ -588,6 +624,28 @@ int cop_coprocessor_poll_async(cop_ctx *ctx, cop_ring *rx, cop_ring *tx, uint32_
 int cop_coprocessor_flush(cop_ctx *ctx, cop_ring *tx, cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats);
 /* The calling thread's context created by coprocessor_setup (or NULL). */
 cop_ctx *coprocessor_ctx(void);
+
+/* The ring loop of several coprocessor threads on ONE poll-mode kernel (the
+ * reference's five coprocessor lcores, each with its own rx ring,
+ * main.c:92-94): cop_pmd_host_create starts a kernel on ctx serving n_rings
+ * rings of n_slots batches of up to max_pkts packets each, whose 16-byte
+ * header records and result records live in mapped pinned host memory (no
+ * launch and no copy per batch), running the drop-in NF chain. Thread r then
+ * calls cop_coprocessor_poll_pmd(h, r, ...) in its loop: it drains up to
+ * max_pkts mbufs from rx, gathers their headers into ring r's next slot and
+ * posts it; it completes (forwards to tx in arrival order, frees drops, as
+ * cop_coprocessor_poll) every batch of the ring already done, oldest first,
+ * and, when rx was empty or every slot is in flight, waits for the oldest.
+ * Returns packets completed or -errno. cop_coprocessor_flush_pmd completes
+ * everything ring r has in flight; cop_pmd_host_destroy (after every ring's
+ * flush) stops the kernel. Ring r is used by one thread. */
+typedef struct cop_pmd_host cop_pmd_host;
+int cop_pmd_host_create(cop_ctx *ctx, uint32_t n_rings, uint32_t max_pkts, uint32_t n_slots, cop_pmd_host **out);
+int cop_coprocessor_poll_pmd(cop_pmd_host *h, uint32_t ring, cop_ring *rx, cop_ring *tx, uint32_t max_pkts,
+                             cop_free_fn free_fn, void *free_arg, cop_nf_stats *stats);
+int cop_coprocessor_flush_pmd(cop_pmd_host *h, uint32_t ring, cop_ring *tx, cop_free_fn free_fn, void *free_arg,
+                              cop_nf_stats *stats);
+int cop_pmd_host_destroy(cop_pmd_host *h);
 
 /* ------------------------------------------------------------------------ */
 /* Deterministic synthetic workload (SURVEY.md §8d generator)               */

@@ -24,7 +24,7 @@ def json_lines(out):
 
 
 def test_spawn_two_ranks_one_line():
-    r = run("--gpus", "2", "--dry-run", "--steps", "20", "--warmup", "5", "--repeats", "3")
+    r = run("--gpus", "2", "--dry-run", "--steps", "20", "--warmup", "5", "--repeats", "3", "--cpu-budget", "0.3")
     assert r.returncode == 0, r.stderr
     lines = json_lines(r.stdout)
     assert len(lines) == 1, r.stdout          # rank 0 only
@@ -37,10 +37,14 @@ def test_spawn_two_ranks_one_line():
     b = 65536
     assert abs(j["value"] - 2 * 20 * b / 1.1e-3 / 1e6) < 1e-3 * j["value"]
     assert ranks[0]["mpkt_s"] > ranks[1]["mpkt_s"]
+    # the CPU baseline rides every N's line (N > 1 lines had none)
+    cb = j["cpu_baseline"]
+    assert cb["cores"] == 1 and cb["kind"] == "port" and cb["value"] > 0 and cb["unit"] == "Mpkt/s"
 
 
 def test_refuses_ranks_sharing_a_gpu():
-    r = run("--gpus", "2", "--dry-run", "--dry-run-devices", "1", "--steps", "4", "--warmup", "0", "--repeats", "1")
+    r = run("--gpus", "2", "--dry-run", "--dry-run-devices", "1", "--steps", "4", "--warmup", "0", "--repeats", "1",
+            "--no-cpu")
     assert r.returncode != 0
     assert "each rank needs its own GPU" in r.stderr
     assert not json_lines(r.stdout)
@@ -48,7 +52,7 @@ def test_refuses_ranks_sharing_a_gpu():
 
 def test_allow_shared_gpu():
     r = run("--gpus", "2", "--dry-run", "--dry-run-devices", "1", "--allow-shared-gpu", "--steps", "4",
-            "--warmup", "0", "--repeats", "1")
+            "--warmup", "0", "--repeats", "1", "--no-cpu")
     assert r.returncode == 0, r.stderr
     j = json_lines(r.stdout)[0]
     assert [x["device"] for x in j["config"]["ranks"]] == [0, 0]
@@ -66,7 +70,8 @@ def test_two_ranks_rule_counter_workload_protocol():
     broadcast from rank 0, the per-interval counter reduction (gloo standing
     in for the RCCL all-reduce) checked and reported — not asserted — and
     each rank's RCCL init status in config.ranks."""
-    r = run("--gpus", "2", "--dry-run", "--workload", "fw_lpm_1m", "--steps", "20", "--warmup", "5", "--repeats", "3")
+    r = run("--gpus", "2", "--dry-run", "--workload", "fw_lpm_1m", "--steps", "20", "--warmup", "5", "--repeats", "3",
+            "--no-cpu")
     assert r.returncode == 0, r.stderr
     lines = json_lines(r.stdout)
     assert len(lines) == 1

@@ -3,8 +3,10 @@
 coprocessor.h:21) -> the firewall stage; DISABLE_NF -> no NF stage (switch.c
 never calls the coprocessor, switch.c:411,426,524; a call anyway forwards
 every packet, as process_packet does without ENABLE_FW_NF, coprocessor.c:59-64).
-The macros live in the caller's build: cop_gpu.h turns coprocessor_setup()
-into cop_coprocessor_setup_stages(COP_DROPIN_STAGES). CPU only: the
+The macros live in the caller's build: cop_gpu.h aliases coprocessor_setup
+to the chain's setup function (cop_coprocessor_setup_fw / _no_nf), an
+object-like macro, so the reference's own `int coprocessor_setup(void);`
+(coprocessor.h:30) still compiles after it. CPU only: the
 preprocessor and the run-time setter (no GPU call)."""
 import os
 import subprocess
@@ -21,6 +23,17 @@ SRC = r'''
 #include <stdio.h>
 int main(void) { printf("%u\n", (unsigned)COP_DROPIN_STAGES); return 0; }
 int use(void) { return coprocessor_setup(); }
+'''
+
+# the reference's coprocessor.h:23-30 declarations after the header, and a
+# function pointer to the setup (ADVICE r3: a function-like macro broke both)
+REF_DECLS = r'''
+#include "cop_gpu.h"
+int coprocessor_setup(void);
+int coprocessor_teardown(void);
+int process_packet(struct rte_mbuf *pkt);
+int (*setup_fn)(void) = &coprocessor_setup;
+int use(void) { return coprocessor_setup() + setup_fn(); }
 '''
 
 
@@ -44,7 +57,22 @@ def expand(tmp_path, *defs):
 def test_macros_select_the_dropin_chain(tmp_path, defs, want):
     val, pre = expand(tmp_path, *defs)
     assert val == want
-    assert "cop_coprocessor_setup_stages(" in pre.split("int use(void)")[1]
+    fn = "cop_coprocessor_setup_no_nf(" if want == 0 else "cop_coprocessor_setup_fw("
+    assert fn in pre.split("int use(void)")[1]
+
+
+@pytest.mark.parametrize("defs", [(), ("ENABLE_FW_NF=1",), ("DISABLE_NF",)])
+def test_reference_declarations_after_header(tmp_path, defs):
+    c = tmp_path / "d.c"
+    c.write_text(REF_DECLS)
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-c", "-o", str(tmp_path / "d.o"),
+                        f"-I{INC}", *[f"-D{d}" for d in defs], str(c)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_chain_setters_exported():
+    L = cg.lib()
+    assert L.cop_coprocessor_setup_fw is not None and L.cop_coprocessor_setup_no_nf is not None
 
 
 def test_runtime_setter():

@@ -344,3 +344,77 @@ def test_no_nf_chain_forwards_everything(rules_file):
     finally:
         assert L.coprocessor_teardown() == 0
         L.cop_set_dropin_stages(cg.STAGE_FW)
+
+
+def test_coprocessor_poll_pmd_rings(rules_file):
+    """Three coprocessor threads, each with its own rx/tx ring pair, on ONE
+    poll-mode kernel (cop_pmd_host_create: the reference's coprocessor lcores
+    each polling its own rx ring, main.c:92-94): per thread the tx_q order
+    equals the oracle's forward list of that thread's packets, every drop is
+    freed exactly once, and nothing is left in flight after the flush."""
+    import threading
+    path, rules = rules_file
+    L = cg.lib()
+    L.cop_set_mbuf_layout(0, 16)
+    L.cop_set_rule_file(path.encode())
+    assert L.coprocessor_setup() == 0
+    try:
+        ctx = L.coprocessor_ctx()
+        R, n, max_pkts = 3, 20000, 4096
+        hp = ctypes.c_void_p()
+        assert L.cop_pmd_host_create(ctx, R, max_pkts, 4, ctypes.byref(hp)) == 0
+        fwo, _ = oracle_tables(rules)
+        FREE = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)
+        res = [None] * R
+
+        def loop(r):
+            pk = cg.gen_trace(0x5EED0620 + r, n, rules)
+            mb = Mbufs(pk, n)
+            _, fo, _ = orc.process(pk, n, stages=DROPIN, fw=fwo)
+            rx = L.cop_ring_create(16384)
+            tx = L.cop_ring_create(65536)
+            freed = []
+            cb = FREE(lambda m, arg: freed.append(mb.index(m)))
+            stats = cg.NfStats()
+            sent = done = polls = 0
+            out = []
+            buf = (ctypes.c_void_p * 256)()
+            while done < n:
+                k_end = min(n, sent + 2500 + 700 * r)
+                while sent < k_end:
+                    k = min(32, k_end - sent)
+                    arr = (ctypes.c_void_p * k)(*[mb.ptr(j) for j in range(sent, sent + k)])
+                    if L.cop_ring_enqueue_bulk(rx, arr, k, None) != k:
+                        break
+                    sent += k
+                got = L.cop_coprocessor_poll_pmd(hp, r, rx, tx, max_pkts, cb, None, ctypes.byref(stats))
+                assert got >= 0, got
+                done += got
+                polls += 1
+                assert polls < 20000
+                while True:
+                    k = L.cop_ring_dequeue_burst(tx, buf, 256, None)
+                    if not k:
+                        break
+                    out += [mb.index(buf[i]) for i in range(k)]
+            assert L.cop_coprocessor_flush_pmd(hp, r, tx, cb, None, ctypes.byref(stats)) == 0
+            while True:
+                k = L.cop_ring_dequeue_burst(tx, buf, 256, None)
+                if not k:
+                    break
+                out += [mb.index(buf[i]) for i in range(k)]
+            L.cop_ring_free(rx)
+            L.cop_ring_free(tx)
+            res[r] = (out == list(fo), sorted(freed) == sorted(set(range(n)) - set(fo)),
+                      stats.tx_packets == len(fo) and stats.tx_dropped == 0)
+
+        th = [threading.Thread(target=loop, args=(r,)) for r in range(R)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(180)
+        assert not any(t.is_alive() for t in th)
+        assert L.cop_pmd_host_destroy(hp) == 0
+        assert res == [(True, True, True)] * R, res
+    finally:
+        L.coprocessor_teardown()

@@ -87,6 +87,57 @@ def test_seg_submit_matches_oracle(gpu_ctx_factory, sizes):
     assert ctx.counters()["rx"] == total
 
 
+@pytest.mark.parametrize("n", [65533, 258, 1])
+def test_seg_lists_write_exactly_n_entries(gpu_ctx_factory, n):
+    """fwd_idx holds n entries, no more: the last segment's list
+    chunk that would reach past entry n-1 is stored word by word. One batch
+    of n (not a multiple of 4) packets with guard words right after its n
+    list entries: one-shot submit, ring launch and poll-mode kernel."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    fw, _ = oracle_tables(rules)
+    pk = cg.gen_trace(0x5EED5E07, n, rules)
+    _, f = oracle_batch(pk, n, S | F, fw)
+    dp = ctx.alloc(pk.nbytes)
+    dp.upload(pk)
+    dr = ctx.alloc(n * 8)
+    dc = ctx.alloc(nseg(n) * 4)
+    guard = 64
+    df = ctx.alloc((n + guard) * 4)
+    df.fill(0xAB)
+    ctx.submit([cg.make_batch(dp, n, dr, fwd_idx=df, fwd_count=dc)])
+    ctx.sync()
+    words = df.download(np.uint32, n + guard)
+    assert np.all(words[n:] == 0xABABABAB), "list stores past entry n-1"
+    assert np.array_equal(seg_to_dense(words[:n], dc.download(np.uint32, nseg(n)), n), f)
+    # ring slots of n packets whose lists sit fwd_slot = n rounded up to 4
+    # words apart: the words between n and fwd_slot stay untouched
+    P, slot = 3, (n + 3) // 4 * 4 + 4
+    pkr = np.tile(pk, P)
+    dpr = ctx.alloc(pkr.nbytes)
+    dpr.upload(pkr)
+    drr = ctx.alloc(P * n * 8)
+    dfr = ctx.alloc(P * slot * 4)
+    dcr = ctx.alloc(P * nseg(n) * 4)
+    ring = cg.make_ring(dpr, P, n, drr, n * 64, fwd_idx=dfr, fwd_slot=slot, fwd_count=dcr)
+    for engine in ("launch", "pmd"):
+        dfr.fill(0xAB)
+        if engine == "launch":
+            ctx.submit_ring(ring, 0, P)
+            ctx.sync()
+        else:
+            with ctx.pmd_start(ring) as m:
+                m.post(P)
+                m.wait()
+        w = dfr.download(np.uint32, P * slot)
+        c = dcr.download(np.uint32, P * nseg(n))
+        for s_ in range(P):
+            assert np.all(w[s_ * slot + n:(s_ + 1) * slot] == 0xABABABAB), f"{engine}: slot {s_} past n"
+            got = seg_to_dense(w[s_ * slot:s_ * slot + n], c[s_ * nseg(n):(s_ + 1) * nseg(n)], n)
+            assert np.array_equal(got, f), f"{engine}: slot {s_}"
+
+
 def test_seg_ring_fw_lpm(gpu_ctx_factory):
     """Ring launches (the bench's form) with the route stage: FW + LPM 100k,
     both DIR-24-8 route probes and LDS firewall intervals."""
@@ -289,3 +340,44 @@ def test_pmd_idle_exit_races_posts(gpu_ctx_factory, monkeypatch, flags):
     m.stop()
     assert ctx.counters()["rx"] == posted * B
     assert launches >= 2   # the idle exits did happen
+
+
+def test_pmd_idle_exit_counts_every_batch_once(gpu_ctx_factory, monkeypatch):
+    """a batch a racing idle exit left half done was redone whole
+    by the relaunch, and its finished tiles' counter and per-rule adds were
+    counted twice. The gate (cop_pmd.hip) now makes an idle exit finish every
+    batch any worker started. Posts race a 2 ms idle limit; per-rule hits by
+    one atomic per hit (COP_HIT_BINS=0: no count kernel, each tile adds its
+    own) and the verdict counters must equal the oracle's exactly."""
+    monkeypatch.setenv("COP_PMD_IDLE_MS", "2")
+    monkeypatch.setenv("COP_HIT_BINS", "0")
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS | cg.CFG_RULE_COUNTERS)
+    tab = cg.LpmTable(rules, 1024, 24, True)
+    ctx.set_fw_table(tab)
+    o = orc.OracleLpm(1024, 24, rules_only=True)
+    o.setup(rules["ip"], rules["depth"], rules["next_hop"])
+    B, P = 65536, 4
+    pk = cg.gen_trace(0x5EED5E41, B * P, rules)
+    per_slot = []
+    for s_ in range(P):
+        h = np.zeros(o.n_rules, np.uint64)
+        orc.process(pk[s_ * B * 64:(s_ + 1) * B * 64], B, stages=S | F, fw=o, rule_hits=h)
+        per_slot.append(h)
+    rg = SegRing(ctx, pk, B, P)
+    m = ctx.pmd_start(rg.ring)
+    posted = 0
+    for i in range(48):
+        time.sleep((1.0 + 0.04 * (i % 51)) * 1e-3 + (0.002 if i % 6 == 5 else 0.0))
+        k = 1 + i % P
+        m.post(k)
+        posted += k
+    m.wait()
+    launches = m.info()["launches"]
+    m.stop()
+    assert launches >= 2
+    assert ctx.counters()["rx"] == posted * B
+    want = np.zeros(o.n_rules, np.uint64)
+    for b in range(posted):
+        want += per_slot[b % P]
+    assert np.array_equal(ctx.rule_counters(), want)

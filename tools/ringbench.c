@@ -18,7 +18,10 @@
  * mbufs are DPDK-shaped (buf_addr at 0, data_off at 16, 2176 B data room,
  * 128 B headroom, init.h:38-44), a pool of 131072 per loop.
  *
- * usage: ringbench <packets per loop> <max_pkts per poll> <loops> [async]
+ * usage: ringbench <packets per loop> <max_pkts per poll> <loops> [async|pmd]
+ *   pmd: every loop's coprocessor thread posts to its own ring of ONE
+ *        poll-mode kernel (cop_pmd_host_create, cop_coprocessor_poll_pmd)
+ *        instead of launching per batch on its own context
  * prints one line: the aggregate Mpkt/s, per-loop rate and batch size;
  * exit 0 when every packet came out of every loop (forwarded + freed).
  * Build: make -C tools ringbench
@@ -34,6 +37,10 @@
 #include <unistd.h>
 
 #include "cop_gpu.h"
+
+/* diagnostics of the library (not in the public header) */
+int cop_debug_dropin_prof(uint64_t *out, uint32_t n, int reset);
+int cop_debug_host_prof(cop_ctx *c, uint64_t *out, uint32_t n, int reset);
 
 #define NB_MBUF 131072u
 #define STRIDE 2176u
@@ -52,13 +59,17 @@ typedef struct loop {
     fake_mbuf *mb;
     uint8_t *data;
     uint64_t n_total, processed, polls, freed;
+    uint64_t prof[7], hprof[6];   /* $COP_HOST_PROF=1: per-op host ns (cop_debug_*_prof) */
     _Atomic uint64_t n_tx;
     atomic_int done, ready;
     int rc;
+    uint32_t id;
 } loop;
 
 static uint32_t g_max_pkts;
 static int g_async;
+static int g_pmd;                 /* loops share one poll-mode kernel, ring l per loop */
+static cop_pmd_host *g_ph;
 static char g_rules[64];
 static atomic_int g_go;
 
@@ -101,6 +112,7 @@ static void *txdrain(void *arg)
 
 static int poll_once(cop_ctx *ctx, loop *L, cop_nf_stats *st)
 {
+    if (g_pmd) return cop_coprocessor_poll_pmd(g_ph, L->id, L->rx, L->tx, g_max_pkts, free_mbuf, L, st);
     return g_async ? cop_coprocessor_poll_async(ctx, L->rx, L->tx, g_max_pkts, free_mbuf, L, st)
                    : cop_coprocessor_poll(ctx, L->rx, L->tx, g_max_pkts, free_mbuf, L, st);
 }
@@ -108,13 +120,13 @@ static int poll_once(cop_ctx *ctx, loop *L, cop_nf_stats *st)
 static void *coprocessor(void *arg)
 {
     loop *L = arg;
-    if (coprocessor_setup() != 0) {
+    if (!g_pmd && coprocessor_setup() != 0) {
         L->rc = 4;
         atomic_store(&L->done, 1);
         atomic_store(&L->ready, 1);
         return NULL;
     }
-    cop_ctx *ctx = coprocessor_ctx();
+    cop_ctx *ctx = coprocessor_ctx();   /* (pmd: unused, the loops share the main thread's kernel) */
     cop_nf_stats st;
     memset(&st, 0, sizeof(st));
     /* warm-up: one small batch through the loop (allocations, first launch) */
@@ -145,8 +157,14 @@ static void *coprocessor(void *arg)
         if (r > 0) L->polls++;
         L->processed += (uint64_t)r;
     }
+    if (g_async && L->rc == 0) cop_coprocessor_flush(ctx, L->tx, free_mbuf, L, &st);
+    if (g_pmd && L->rc == 0) cop_coprocessor_flush_pmd(g_ph, L->id, L->tx, free_mbuf, L, &st);
     atomic_store(&L->done, 1);
-    coprocessor_teardown();
+    cop_debug_dropin_prof(L->prof, 7, 1);
+    if (!g_pmd) {
+        cop_debug_host_prof(ctx, L->hprof, 6, 1);
+        coprocessor_teardown();
+    }
     return NULL;
 }
 
@@ -167,7 +185,8 @@ int main(int argc, char **argv)
     g_max_pkts = (uint32_t)strtoul(argv[2], NULL, 0);
     const int nl = atoi(argv[3]);
     g_async = argc > 4 && strcmp(argv[4], "async") == 0;
-    if (nl < 1 || nl > MAX_LOOPS) return 2;
+    g_pmd = argc > 4 && strcmp(argv[4], "pmd") == 0;
+    if (nl < 1 || nl > MAX_LOOPS || (g_pmd && nl > COP_PMD_MAX_RINGS)) return 2;
 
     /* rules.json in the reference format, read by the reference's setup path */
     cop_prefix *rules = calloc(1000, sizeof(cop_prefix));
@@ -177,6 +196,15 @@ int main(int argc, char **argv)
     cop_set_rule_file(g_rules);   /* process-wide, before any coprocessor thread */
     cop_set_mbuf_layout(0, 16);
 
+    if (g_pmd) {
+        /* one context (the main thread's) and one kernel for every loop */
+        if (coprocessor_setup() != 0) return 4;
+        int prc = cop_pmd_host_create(coprocessor_ctx(), (uint32_t)nl, g_max_pkts, 4, &g_ph);
+        if (prc) {
+            fprintf(stderr, "cop_pmd_host_create: %d %s\n", prc, cop_last_error(coprocessor_ctx()));
+            return 4;
+        }
+    }
     uint8_t *trace = malloc((size_t)NB_MBUF * 64);
     if (!trace || cop_gen_trace(0x5EED0002, NB_MBUF, NULL, rules, 1000, NULL, 0, trace, 64) != 0) return 7;
     static loop loops[MAX_LOOPS];
@@ -184,6 +212,7 @@ int main(int argc, char **argv)
     for (int l = 0; l < nl; l++) {
         loop *L = &loops[l];
         L->n_total = per_loop;
+        L->id = (uint32_t)l;
         L->data = malloc((size_t)NB_MBUF * STRIDE);
         L->mb = calloc(NB_MBUF, sizeof(fake_mbuf));
         L->rx = cop_ring_create(COP_NF_QUEUE_RINGSIZE);
@@ -224,8 +253,27 @@ int main(int argc, char **argv)
         polls += L->polls;
     }
     remove(g_rules);
+    if (g_pmd) {
+        cop_pmd_host_destroy(g_ph);
+        coprocessor_teardown();
+    }
+    if (getenv("COP_HOST_PROF")) {
+        /* loop 0's host time per packet, by op (ns/pkt), and per busy call (us) */
+        loop *L = &loops[0];
+        const double pk = L->prof[6] ? (double)L->prof[6] : 1.0;
+        const double calls = L->prof[5] ? (double)L->prof[5] : 1.0;
+        printf("prof loop0 %s: ns/pkt drain %.2f batch %.2f wait %.2f fwd %.2f | calls %llu busy %llu pkts %llu "
+               "(%.0f pkts/busy call, %.1f us/busy call) | host batch ns/pkt gather %.2f launch %.2f wait %.2f "
+               "copy %.2f (%llu batches, %.1f us launch/batch, %.1f us wait/batch)\n",
+               g_pmd ? "pmd" : g_async ? "async" : "sync", L->prof[0] / pk, L->prof[1] / pk, L->prof[2] / pk, L->prof[3] / pk,
+               (unsigned long long)L->prof[4], (unsigned long long)L->prof[5], (unsigned long long)L->prof[6],
+               L->prof[6] / calls, (L->prof[0] + L->prof[1] + L->prof[2] + L->prof[3]) / calls / 1e3,
+               L->hprof[0] / pk, L->hprof[1] / pk, L->hprof[2] / pk, L->hprof[3] / pk,
+               (unsigned long long)L->hprof[4], L->hprof[4] ? L->hprof[1] / (double)L->hprof[4] / 1e3 : 0.0,
+               L->hprof[4] ? L->hprof[2] / (double)L->hprof[4] / 1e3 : 0.0);
+    }
     printf("%s loops %2d max_pkts %6u  %8.1f Mpkt/s aggregate (%.1f per loop), %.0f pkts per poll\n",
-           g_async ? "async" : "sync ", nl, g_max_pkts, (double)total / dt / 1e6, (double)total / dt / 1e6 / nl,
+           g_pmd ? "pmd  " : g_async ? "async" : "sync ", nl, g_max_pkts, (double)total / dt / 1e6, (double)total / dt / 1e6 / nl,
            polls ? (double)total / (double)polls : 0.0);
     return rc;
 }
