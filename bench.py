@@ -218,6 +218,15 @@ def table_probes(fw_tab, rt_tab, sample, imix_offsets, route_form):
         if form == "trie":
             out[name] = {"form": "trie (LDS top level, L2 nodes)", "global_probes_per_pkt": None}
             continue
+        if form == "bkt":
+            # one 8-byte index load + one 16-byte pair load per reaching
+            # packet, plus the wide-bucket rounds (two 16-byte loads each)
+            _, _, info = tab.bkt_probe(key[reach], 0)
+            out[name] = {"form": "bkt (bucketed intervals, L2)", "ib": info["ib"],
+                         "l2_loads_per_pkt": round((2 * float(reach.sum()) + 2 * info["rounds"]) / n, 4),
+                         "wide_lookups_per_pkt": round(info["lifted"] / n, 4),
+                         "table_bytes": ((1 << info["ib"]) + 1) * 4 + (info["m"] + 4) * 8}
+            continue
         t24, _ = tab.dir24()
         e = t24[key[reach] >> 8]
         ext = ((e & 0x03000000) == 0x03000000).sum()
@@ -271,7 +280,7 @@ def measure(args, name, rank, world, dev, group, primary):
     seg = args.lists == "seg"
     ctx = cg.Context(device=dev, stages=stages, max_batch=B, max_batches=32, n_streams=args.streams,
                      flags=(cg.CFG_RULE_COUNTERS if rc_on else 0) | (cg.CFG_NO_COMPACT if args.no_compact else 0)
-                     | (cg.CFG_LPM_TRIE if args.route_form == "trie" else 0)
+                     | {"dir": 0, "trie": cg.CFG_LPM_TRIE, "bkt": cg.CFG_LPM_BKT}[args.route_form]
                      | (cg.CFG_SEG_LISTS if seg else 0))
     ctx.set_fw_table(fw_tab)
     coll = None
@@ -635,9 +644,10 @@ def main():
     ap.add_argument("--lists", default="seg", choices=("seg", "dense"),
                     help="ordered forward lists: seg = 256-packet segments (COP_CFG_SEG_LISTS: per-segment "
                          "lists + counts, no cross-tile prefix), dense = one list per batch (decoupled look-back)")
-    ap.add_argument("--route-form", default="dir", choices=("dir", "trie"),
+    ap.add_argument("--route-form", default="dir", choices=("dir", "trie", "bkt"),
                     help="route tables too large for LDS: DIR-24-8 image (HBM / Infinity Cache) or the multibit "
-                         "trie (12-bit LDS top level + L2-resident 6-bit nodes)")
+                         "trie (12-bit LDS top level + L2-resident 6-bit nodes) or the bucketed intervals "
+                         "(index + (start, value) pairs in L2: two loads per lookup)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

@@ -25,6 +25,7 @@ COUNTER_SHARDS = 256   # COP_COUNTER_SHARDS
 LPM_STOP_AT_FIRST_ERROR = 0x1
 CFG_FW_FORCE_DIR24, CFG_LPM_FORCE_DIR24, CFG_NO_COMPACT, CFG_RULE_COUNTERS = 0x1, 0x2, 0x4, 0x8
 CFG_DEMUX_PORTS, CFG_PORT_STATS, CFG_LPM_TRIE, CFG_SEG_LISTS = 0x10, 0x20, 0x40, 0x80
+CFG_LPM_BKT = 0x100
 SEG_PKTS = 256   # COP_SEG_PKTS: packets per forward-list segment (CFG_SEG_LISTS)
 MAX_DEMUX_PORTS = 8
 GEN_FW, GEN_ROUTES = 0, 1
@@ -158,6 +159,7 @@ SIGNATURES = {
     "cop_dev_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
     "cop_dev_free": (c_int, [c_void_p, c_void_p]),
     "cop_host_alloc_pinned": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    "cop_host_alloc_mapped": (c_int, [c_void_p, c_size_t, POINTER(c_void_p), POINTER(c_void_p)]),
     "cop_host_free_pinned": (c_int, [c_void_p, c_void_p]),
     "cop_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
     "cop_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
@@ -216,6 +218,8 @@ def lib():
             raise ImportError(f"{path} not built (run make -C ghost-dataplane_amd)")
         L = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("COP_LIB") and not hasattr(L, name):
+                continue   # an older A/B build: calls it lacks fail when used
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
@@ -390,6 +394,20 @@ class LpmTable:
                what="cop_lpm_trie_probe")
         return out, ref, nn.value, nl.value
 
+    def bkt_probe(self, ips: np.ndarray, form: int = 0, xbits: int = 1):
+        """The bucketed interval form (lpm_bkt.c) of this table's device
+        image (form 0: next hop, 1: rule id), looked up on the host the way
+        the kernel does: (values, interval-search values, info dict)."""
+        ips = np.ascontiguousarray(ips, dtype=np.uint32)
+        out = np.zeros(len(ips), dtype=np.uint32)
+        ref = np.zeros(len(ips), dtype=np.uint32)
+        info = np.zeros(6, dtype=np.uint32)
+        f = lib().cop_lpm_bkt_probe
+        f.restype = c_int
+        f.argtypes = [c_void_p, c_int, c_uint32, c_void_p, c_uint32, c_void_p, c_void_p, c_void_p]
+        _check(f(self.handle, form, xbits, _ptr(ips), len(ips), _ptr(out), _ptr(ref), _ptr(info)), what="cop_lpm_bkt_probe")
+        return out, ref, dict(zip(("m", "ib", "lv", "widest", "lifted", "rounds"), (int(x) for x in info)))
+
     def dir24(self):
         t24 = np.zeros(1 << 24, dtype=np.uint32)
         cap = 256 * max(1, self.report.n_distinct)
@@ -504,6 +522,16 @@ class Context:
 
     def set_route_lpm(self, t: LpmTable):
         _check(lib().cop_set_route_lpm(self.handle, t.handle), self, "set_route_lpm")
+
+    ROUTE_FORMS = {1: "lds", 2: "dir", 3: "trie", 4: "bkt"}
+
+    def route_form(self) -> str:
+        """The route stage's table form a launch uses now (lds: LDS
+        intervals, dir: DIR-24-8, trie, bkt: bucketed intervals in L2)."""
+        f = lib().cop_debug_route_form
+        f.restype = c_int
+        f.argtypes = [c_void_p]
+        return self.ROUTE_FORMS[_check(f(self.handle), self, "route_form")]
 
     def set_routing_table(self, rt: np.ndarray):
         rt = np.ascontiguousarray(rt, dtype=np.uint16)

@@ -442,6 +442,20 @@ __device__ __forceinline__ uint32_t probe_ld(const uint32_t *a, uint32_t nt)
     return nt ? __builtin_nontemporal_load(a) : *a;
 }
 
+// The bucketed route form's first round (COPK_TBL_BKT): the bucket's first
+// candidate and the next bucket's (both issued, not waited for)
+__device__ __forceinline__ void bkt_issue(const uint32_t *bidx, uint32_t ib, uint32_t ip, bool reach, uint32_t &k0,
+                                          uint32_t &k1)
+{
+    if (reach) {
+        const u32x2a x = *(const u32x2a *)(bidx + (ip >> (32u - ib)));
+        k0 = x.x;
+        k1 = x.y;
+    } else {
+        k0 = k1 = 0;
+    }
+}
+
 // Pass 1, per step: parse, vport route (stage P), interval searches in LDS,
 // and the tbl24 loads of DIR-24-8 stages (issued, not waited for).
 // w3 = bytes 12..15, w6/w7/w8 = bytes 24..35 of the packet as loaded (LE).
@@ -450,7 +464,7 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
                                       const uint32_t (&w6)[PPT], const uint32_t (&w7)[PPT],
                                       const uint32_t (&w8)[PPT], uint32_t (&verdict)[PPT], uint32_t (&port)[PPT],
                                       uint32_t (&src)[PPT], uint32_t (&dst)[PPT], uint32_t (&fwe)[PPT],
-                                      uint32_t (&lpe)[PPT])
+                                      uint32_t (&lpe)[PPT], uint32_t (&lpe2)[PPT])
 {
     const bool stageP = (p.stages & COPK_STAGE_PARSE) != 0;
 #pragma unroll
@@ -481,6 +495,7 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
         if (LPM == COPK_TBL_IVT) lpe[k] = t.lp_v[ivt_search(t.lp_s, p.lpm_m, p.lpm_ib, p.lpm_lv, dst[k])];
         if (LPM == COPK_TBL_DIR) lpe[k] = reach ? probe_ld(&p.lpm_tbl24[dst[k] >> 8], p.probe_nt) : 0u;
         if (LPM == COPK_TBL_TRIE) lpe[k] = t.lp_s[dst[k] >> 20];
+        if (LPM == COPK_TBL_BKT) bkt_issue(p.lpm_bidx, p.lpm_ib, dst[k], reach, lpe[k], lpe2[k]);
     }
 }
 
@@ -572,6 +587,62 @@ __device__ __forceinline__ void tbl8_step(const uint32_t *tbl8, uint32_t packed,
     }
 }
 
+// The bucketed route form's second round (COPK_TBL_BKT, lpm_bkt.c): for
+// each reached packet with candidates k0..k1 (start k0 <= ip, R(ip) <= k1),
+// one 16-byte load of pairs k0 and k0 + 1 decides when ip is below start
+// k0 + 1 or k1 <= k0 + 1 (all PPT loads issued before any is used). Lanes in
+// a wider bucket then scan on, four pairs (two 16-byte loads) a round, until
+// a start above ip or k1: a wave that holds any such lane pays about one
+// more round, not a binary search's lv dependent loads.
+// e[k] <- the interval's value (the rte_lpm entry form: bit 24 hit, nh).
+template <int PPT>
+__device__ __forceinline__ void bkt_step(const uint32_t *pairs, const uint32_t (&ip)[PPT], uint32_t (&e)[PPT],
+                                         const uint32_t (&k1)[PPT], const bool (&live)[PPT])
+{
+    u32x4a q[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; k++)
+        if (live[k]) q[k] = *(const u32x4a *)(pairs + 2 * (size_t)e[k]);
+    bool more[PPT];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+        more[k] = false;
+        if (!live[k]) continue;
+        const uint32_t k0 = e[k];
+        const bool up = ip[k] >= q[k].z;   // start k0 + 1 (a pad of 0xFFFFFFFF past the end)
+        more[k] = up && k1[k] > k0 + 1u;
+        any |= more[k];
+        e[k] = up ? q[k].w : q[k].y;
+        if (more[k]) q[k].x = k0 + 2u;     // the next pair to look at
+    }
+    // the rare wide bucket: pairs j .. j + 3 per round (pads past the end
+    // hold start 0xFFFFFFFF; j <= k1 <= m - 1, so j + 3 < m + 4)
+    while (__ballot(any)) {
+        u32x4a a[PPT], b[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            if (more[k]) {
+                a[k] = *(const u32x4a *)(pairs + 2 * (size_t)q[k].x);
+                b[k] = *(const u32x4a *)(pairs + 2 * (size_t)q[k].x + 4);
+            }
+        }
+        any = false;
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            if (!more[k]) continue;
+            const uint32_t j = q[k].x, hi = k1[k];
+            if (ip[k] >= a[k].x) e[k] = a[k].y;                       // j <= k1 always
+            if (j + 1u <= hi && ip[k] >= a[k].z) e[k] = a[k].w;
+            if (j + 2u <= hi && ip[k] >= b[k].x) e[k] = b[k].y;
+            if (j + 3u <= hi && ip[k] >= b[k].z) e[k] = b[k].w;
+            more[k] = j + 3u < hi && ip[k] >= b[k].z;
+            any |= more[k];
+            q[k].x = j + 4u;
+        }
+    }
+}
+
 // Pass 2: rte_lpm_lookup's tbl8 step for valid+extended entries, then the
 // verdicts of stage FW (firewall.c:183-210) and stage LPM. Packets that did
 // not reach the coprocessor (stage P drop) keep their verdict. Counts the
@@ -579,8 +650,9 @@ __device__ __forceinline__ void tbl8_step(const uint32_t *tbl8, uint32_t packed,
 template <int FW, int LPM, int PPT>
 __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[PPT], const uint32_t (&src)[PPT],
                                       const uint32_t (&dst)[PPT], const bool (&valid)[PPT], uint32_t (&fwe)[PPT],
-                                      uint32_t (&lpe)[PPT], uint32_t (&verdict)[PPT], uint32_t (&flags)[PPT],
-                                      uint32_t (&rnh)[PPT], uint32_t &c_total, uint32_t &c_notv4)
+                                      uint32_t (&lpe)[PPT], const uint32_t (&lpe2)[PPT], uint32_t (&verdict)[PPT],
+                                      uint32_t (&flags)[PPT], uint32_t (&rnh)[PPT], uint32_t &c_total,
+                                      uint32_t &c_notv4)
 {
     bool reached[PPT];
 #pragma unroll
@@ -592,6 +664,7 @@ __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[
     if (FW == COPK_TBL_DIR) tbl8_step<PPT>(p.fw_tbl8, p.fw_tbl8_packed, src, fwe);
     if (LPM == COPK_TBL_DIR) tbl8_step<PPT>(p.lpm_tbl8, p.lpm_tbl8_packed, dst, lpe);
     if (LPM == COPK_TBL_TRIE) trie_walk<PPT>(p.lpm_tnodes, p.lpm_tleaves, dst, lpe, reached);
+    if (LPM == COPK_TBL_BKT) bkt_step<PPT>(p.lpm_bpairs, dst, lpe, lpe2, reached);
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         if (!reached[k]) continue;

@@ -87,6 +87,30 @@ uint32_t cop_lpm_trie_lookup(const cop_lpm_trie *t, uint32_t ip);
 int cop_lpm_trie_probe(const cop_lpm_table *tab, int form, const uint32_t *ips, uint32_t n, uint32_t *out,
                        uint32_t *ref, uint32_t *n_nodes, uint32_t *n_leaves);
 
+/* Bucketed interval device form (lpm_bkt.c, COP_CFG_LPM_BKT): idx = 2^ib + 1
+ * first-candidate positions, pairs = (start, value) x (m + COP_BKT_PADS) */
+#define COP_BKT_MIN_BITS 12u
+#define COP_BKT_MAX_BITS 22u
+#define COP_BKT_PADS 4u
+#define COP_BKT_XBITS 1u   /* default: 2 buckets per interval */
+typedef struct {
+    uint32_t m, ib, lv, widest;
+    uint32_t *idx;
+    uint32_t *pairs;
+} cop_lpm_bkt;
+int cop_lpm_bkt_build(const uint32_t *starts, const uint32_t *vals, uint32_t m, uint32_t xbits, cop_lpm_bkt *out);
+void cop_lpm_bkt_free(cop_lpm_bkt *t);
+uint32_t cop_lpm_bkt_lookup(const cop_lpm_bkt *t, uint32_t ip, uint32_t *rounds);
+/* tests: the bucketed form of a table's form; per ip its lookup (out) and
+ * the binary search over all intervals (ref); info = {m, ib, lv, widest,
+ * lookups that needed a wide-bucket round, the wide-bucket rounds} */
+int cop_lpm_bkt_probe(const cop_lpm_table *tab, int form, uint32_t xbits, const uint32_t *ips, uint32_t n,
+                      uint32_t *out, uint32_t *ref, uint32_t *info);
+
+/* tests: the route stage's table form a launch would use (COPK_TBL_*: 1 LDS
+ * intervals, 2 DIR-24-8, 3 trie, 4 bucketed) */
+int cop_debug_route_form(cop_ctx *c);
+
 /* Host paths with an explicit stage mask instead of the context's: the
  * drop-in coprocessor API (dropin.c) runs the coprocessor thread's NF chain,
  * COP_DROPIN_STAGES (process_packet, coprocessor.c:50-65). */
@@ -101,9 +125,6 @@ int cop_host_batch_submit_stages(cop_ctx *c, uint32_t stages, uint32_t slot, con
 typedef struct cop_pmd cop_pmd;
 int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t n_rings, uint32_t flags,
                                uint32_t stages, cop_pmd **out);
-/* Mapped pinned host memory: *hptr for the host, *dptr the device's address
- * of the same bytes (free with cop_host_free_pinned). */
-int cop_host_alloc_mapped(cop_ctx *c, size_t bytes, void **hptr, void **dptr);
 
 /* Diagnostics ($COP_HOST_PROF=1): host ns per op of the host batch paths of
  * a context: [0] gather, [1] launch, [2] wait, [3] copy-out, [4] batches,

@@ -22,6 +22,8 @@ static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_TBL_IVT 1  /* flattened intervals, binary search in LDS */
 #define COPK_TBL_DIR 2  /* DIR-24-8 image in HBM */
 #define COPK_TBL_TRIE 3 /* multibit trie: 12-bit top level in LDS, 6-bit popcount nodes in L2 (route stage) */
+#define COPK_TBL_BKT 4  /* bucketed intervals in global memory (L2): first candidate per top-ib-bit bucket,
+                           then (start, value) pairs (route stage) */
 #define COPK_TRIE_L0 4096u
 /* Packed tbl8 form of a DIR-24-8 image: an extended tbl24 entry's payload is
  * the offset (in 64-byte units) of its /24's run block instead of a group
@@ -107,6 +109,12 @@ struct CopKParams {
     const uint32_t *lpm_tl0;     // trie form (lpm_trie.c): 4096 top entries (staged in LDS)
     const uint32_t *lpm_tnodes;  // 6 u32 per node: vec, leafvec (u64 each), child_base, leaf_base
     const uint32_t *lpm_tleaves;
+    // bucketed form (COPK_TBL_BKT): lpm_bidx[b] = the last interval k with
+    // start <= b << (32 - lpm_ib), b in [0, 2^lpm_ib] (the last entry: m - 1);
+    // lpm_bpairs[2k] = start k, [2k + 1] = its value (padded with four
+    // {0xFFFFFFFF, last value} pairs); lpm_lv lifting levels above the
+    // widest bucket
+    const uint32_t *lpm_bidx, *lpm_bpairs;
     // LDS carve (u32 words)
     uint32_t lds_fw_off, lds_lpm_off, lds_misc_off;
     uint32_t lds_stage_off;   // one-shot kernel: the tile's forward list staged in LDS (0: none)
@@ -158,7 +166,7 @@ struct CopKPmd {
     const uint32_t *h_n;
     unsigned long long *d_act;           // device: s_memrealtime of the last doorbell change of any ring
     const unsigned long long *h_posted;  // host-mapped: batches posted (monotonic), ring r's at [8 r]
-    const uint32_t *h_stop;              // host-mapped: non-zero = leave once idle
+    const uint32_t *h_stop;              // host-mapped: 1 = stop, 2 = pause (leave, to be relaunched)
     // host-mapped completion: [r * n_slots + slot] = sequence + 1 of its
     // last completed batch, written by the slot's last tile (every output
     // byte of the batch, and its counter adds, landed before)
@@ -182,6 +190,7 @@ struct CopKPmd {
     uint32_t n_work;                     // worker workgroups
     uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
     uint32_t stepwise;                   // tiles step by step where tile_steps applies ($COP_PMD_STEPWISE=0: off)
+    uint32_t prefetch;                   // L2 prefetch of the next posted tile's first steps ($COP_PMD_PREFETCH)
     uint32_t poll_backoff;               // waiting workers' s_sleep(4) rounds between relay polls once idle
                                          // (3: ~0.3 us, the default; 0: busy polling, $COP_PMD_BACKOFF)
 };
@@ -191,6 +200,7 @@ struct CopKPmd {
 #define COPK_PMD_STOPPED 1u   /* the host asked (cop_pmd_stop) */
 #define COPK_PMD_IDLE 2u      /* no post for idle_ticks: left; the next post relaunches */
 #define COPK_PMD_ABORT 3u     /* not every worker became resident, or a look-back timed out */
+#define COPK_PMD_PAUSED 4u    /* the host asked it to make room for other kernels; relaunched after */
 
 #ifdef __cplusplus
 extern "C" {

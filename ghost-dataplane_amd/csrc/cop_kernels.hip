@@ -154,6 +154,7 @@ hipError_t launch_lpm(const CopKParams &p, int lpm, int imix, int ppt, uint32_t 
     if (lpm == COPK_TBL_IVT) return launch_imix<FW, COPK_TBL_IVT>(p, imix, ppt, grid, lds, s);
     if (lpm == COPK_TBL_DIR) return launch_imix<FW, COPK_TBL_DIR>(p, imix, ppt, grid, lds, s);
     if (lpm == COPK_TBL_TRIE) return launch_imix<FW, COPK_TBL_TRIE>(p, imix, ppt, grid, lds, s);
+    if (lpm == COPK_TBL_BKT) return launch_imix<FW, COPK_TBL_BKT>(p, imix, ppt, grid, lds, s);
     return launch_imix<FW, COPK_TBL_OFF>(p, imix, ppt, grid, lds, s);
 }
 

@@ -48,6 +48,12 @@ __device__ __forceinline__ uint32_t ld_agent(uint32_t *p)
 }
 
 constexpr unsigned long long GATE_POSTED = (1ull << COPK_PMD_GATE_SHIFT) - 1ull;
+// experiment builds only: COPK_PMD_NOGATE=1 relays without publishing
+// through the gate (timing of the gate's CAS on the doorbell path; exits may
+// then leave batches half done)
+#ifndef COPK_PMD_NOGATE
+#define COPK_PMD_NOGATE 0
+#endif
 
 __device__ __forceinline__ unsigned long long ld_u64(const unsigned long long *p)
 {
@@ -115,7 +121,12 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
         const unsigned long long hp = ld_u64(relay);
         const uint32_t ex = ld_agent(&P.d_ctl[0]);
         unsigned long long h = 0;
-        if (leader) h = __hip_atomic_load(h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t stop = 0;
+        if (leader) {
+            // the doorbell and the stop word in one PCIe round trip
+            h = __hip_atomic_load(h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            stop = __hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         if (hp > b) return hp;
         if (ex) {
             if (ex == COPK_PMD_ABORT) return 0;
@@ -128,7 +139,7 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
         }
         if (leader) {
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-            if (h > hp && gate_publish(gate, h)) {
+            if (h > hp && (COPK_PMD_NOGATE || gate_publish(gate, h))) {
                 for (int x = 0; x < COPK_PMD_RELAYS; x++) atomicMax(relays + x * 16, h);
                 if (P.stamps && r == 0) {   // diagnostic: when each doorbell value was relayed
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2], h);
@@ -141,13 +152,13 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
                 t_seen = now;
                 if (P.n_rings > 1) atomicMax(P.d_act, now);   // activity on this ring keeps every ring's kernel up
             }
-            // the exit checks every 16th poll: the stop flag is a second
-            // PCIe read, and the doorbell is polled once per round trip
-            if ((spins & 15u) == 15u) {
+            // stop or pause at once (the host waits for them); a look-back
+            // timeout and the idle clock every 16th poll
+            if (stop) {
+                pmd_leave(P, stop == 2u ? COPK_PMD_PAUSED : COPK_PMD_STOPPED);
+            } else if ((spins & 15u) == 15u) {
                 if (ld_agent(&P.d_ctl[2])) {
                     pmd_leave(P, COPK_PMD_ABORT);   // a look-back timed out
-                } else if (__hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
-                    pmd_leave(P, COPK_PMD_STOPPED);
                 } else {
                     unsigned long long last = t_seen;
                     if (P.n_rings > 1) last = max(last, ld_u64(P.d_act));
@@ -181,6 +192,11 @@ __device__ __forceinline__ __attribute__((unused)) CopKBatch pmd_batch(const Cop
     return B;
 }
 
+// experiment builds only: COPK_PMD_PF=1 compiles the next-tile L2 prefetch
+// ($COP_PMD_PREFETCH=1 turns it on; its registers spill in production builds)
+#ifndef COPK_PMD_PF
+#define COPK_PMD_PF 0
+#endif
 // experiment builds only: COPK_PMD_WT=0 stores non-temporally (timing of the
 // write-through cost; results are then not guaranteed visible at completion)
 #ifndef COPK_PMD_WT
@@ -296,9 +312,31 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             }
             // tile_steps stores records from lane pairs only (p.rec_paired: every
             // slot's records 16-byte aligned); other record forms take tile_body
-            if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && p.rec_paired && P.stepwise)
-                tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, B, j, tid_i, lane_i, wave_i);
-            else
+            if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && p.rec_paired && P.stepwise) {
+                // experiment ($COP_PMD_PREFETCH): once this tile's loads are
+                // out, one plain load per lane of each 128-byte line of the
+                // first two steps of this worker's next tile, if posted, so
+                // its headers sit in L2 when its own loads go out. The value
+                // is consumed after the tile (its wait joins the drain).
+                uint32_t pfv = 0;
+                auto pf = [&] {
+                    if (!COPK_PMD_PF || !P.prefetch) return;
+                    uint32_t j2 = j + rb;
+                    unsigned long long b2 = b + qb;
+                    if (j2 >= tpb) {
+                        j2 -= tpb;
+                        b2++;
+                    }
+                    if (b2 >= posted || P.h_n) return;
+                    uint32_t s2 = slot + (uint32_t)((b2 - b) % n_slots);
+                    if (s2 >= n_slots) s2 -= n_slots;
+                    const uint8_t *pk2 = rg.pkts + (size_t)s2 * rg.pkts_slot_bytes + rg.data_off;
+                    const uint32_t pkt = min(j2 * TILE + (uint32_t)tid_i * 2u, rg.n - 1u);
+                    pfv = *(const uint32_t *)(pk2 + (size_t)pkt * rg.stride);
+                };
+                tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, B, j, tid_i, lane_i, wave_i, pf);
+                if (COPK_PMD_PF) asm volatile("" ::"v"(pfv));
+            } else
                 ok = tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
                     p, o, lc, B, look_off, j, LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0]}, tid_i,
                     lane_i, wave_i, false, (size_t)(rs0 + slot) * tpb + j);
@@ -372,6 +410,7 @@ hipError_t pmd_lpm(const CopKPmd *p, int lpm, int lay, int ppt, int ext, uint32_
     if (lpm == COPK_TBL_IVT) return pmd_lay<FW, COPK_TBL_IVT>(p, lay, ppt, ext, lds, s, occ);
     if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);
     if (lpm == COPK_TBL_TRIE) return pmd_lay<FW, COPK_TBL_TRIE>(p, lay, ppt, ext, lds, s, occ);
+    if (lpm == COPK_TBL_BKT) return pmd_lay<FW, COPK_TBL_BKT>(p, lay, ppt, ext, lds, s, occ);
     return pmd_lay<FW, COPK_TBL_OFF>(p, lay, ppt, ext, lds, s, occ);
 }
 

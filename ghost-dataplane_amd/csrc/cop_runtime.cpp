@@ -55,6 +55,11 @@ struct DevLpm {
     // multibit-trie form (lpm_trie.c): top level, nodes, leaves; null if not built
     uint32_t *tl0 = nullptr, *tnodes = nullptr, *tleaves = nullptr;
     uint32_t t_nodes = 0, t_leaves = 0;
+    // bucketed global form (COP_CFG_LPM_BKT; m == 0, ib / lv its own):
+    // bidx = 2^ib + 1 first-candidate positions, bpairs = (start, value)
+    // pairs padded with four {0xFFFFFFFF, last value}; null if not built
+    uint32_t *bidx = nullptr, *bpairs = nullptr;
+    uint32_t b_m = 0;
 };
 
 struct Lane {
@@ -184,6 +189,7 @@ struct cop_ctx {
     bool static_small = true;  // small launches in blockIdx tile order ($COP_STATIC_ORDER=0: tickets)
     bool rec_paired = false;   // one-shot kernel: records as 16-byte stores from lane pairs ($COP_REC_PAIRED=1)
     bool probe_nt = false;     // tbl24 probes as non-temporal loads ($COP_PROBE_NT=1, experiment)
+    uint32_t bkt_xbits = COP_BKT_XBITS;   // bucketed route form: 2^x buckets per interval ($COP_BKT_XBITS)
     uint32_t dbg = 0;          // $COP_DBG: timing-only kernel ablations
     uint32_t lds_pad = 0;      // $COP_LDS_PAD: extra LDS bytes per workgroup (occupancy experiments)
     unsigned long long *stamps = nullptr;   // dbg bit 8: per-workgroup phase stamps
@@ -332,6 +338,8 @@ static void free_lpm(DevLpm &t)
     if (t.tl0) (void)hipFree(t.tl0);
     if (t.tnodes) (void)hipFree(t.tnodes);
     if (t.tleaves) (void)hipFree(t.tleaves);
+    if (t.bidx) (void)hipFree(t.bidx);
+    if (t.bpairs) (void)hipFree(t.bpairs);
     t = DevLpm();
 }
 
@@ -519,10 +527,12 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_STATIC_ORDER")) c->static_small = atoi(e) != 0;
     if (const char *e = getenv("COP_REC_PAIRED")) c->rec_paired = atoi(e) != 0;
     if (const char *e = getenv("COP_PROBE_NT")) c->probe_nt = atoi(e) != 0;
+    if (const char *e = getenv("COP_BKT_XBITS")) c->bkt_xbits = (uint32_t)atoi(e) & 7u;
     // route-table form for tables too large for LDS (A/B runs): trie | dir
     if (const char *e = getenv("COP_LPM_FORM")) {
-        if (!strcmp(e, "trie")) c->cfg.flags |= COP_CFG_LPM_TRIE;
-        else if (!strcmp(e, "dir")) c->cfg.flags &= ~COP_CFG_LPM_TRIE;
+        if (!strcmp(e, "trie")) c->cfg.flags = (c->cfg.flags & ~COP_CFG_LPM_BKT) | COP_CFG_LPM_TRIE;
+        else if (!strcmp(e, "bkt")) c->cfg.flags = (c->cfg.flags & ~COP_CFG_LPM_TRIE) | COP_CFG_LPM_BKT;
+        else if (!strcmp(e, "dir")) c->cfg.flags &= ~(COP_CFG_LPM_TRIE | COP_CFG_LPM_BKT);
     }
     if (const char *e = getenv("COP_STREAMS")) {
         int v = atoi(e);
@@ -663,7 +673,28 @@ static int upload_trie(cop_ctx *c, DevLpm &t, const uint32_t *s, const uint32_t 
     return 0;
 }
 
-static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt, int form, bool want_trie = false)
+// the bucketed global form of intervals (s, v, m) into t (COP_CFG_LPM_BKT;
+// lpm_bkt.c)
+static int upload_bkt(cop_ctx *c, DevLpm &t, const uint32_t *s, const uint32_t *v, uint32_t m)
+{
+    cop_lpm_bkt bk;
+    int rc = cop_lpm_bkt_build(s, v, m, c->bkt_xbits, &bk);
+    if (rc) return set_err(c, rc, "bucketed route form build failed: %d", rc);
+    const size_t ib = ((size_t)(1u << bk.ib) + 1) * 4, pb = 2 * ((size_t)m + COP_BKT_PADS) * 4;
+    hipError_t e = hipMalloc(&t.bidx, ib);
+    if (e == hipSuccess) e = hipMalloc(&t.bpairs, pb);
+    if (e == hipSuccess) e = hipMemcpy(t.bidx, bk.idx, ib, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(t.bpairs, bk.pairs, pb, hipMemcpyHostToDevice);
+    t.ib = bk.ib;
+    t.lv = bk.lv;
+    t.b_m = m;
+    cop_lpm_bkt_free(&bk);
+    if (e != hipSuccess) return set_err(c, -ENOMEM, "bucketed route form upload: %s", hipGetErrorString(e));
+    return 0;
+}
+
+static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want_ivt, int form, bool want_trie = false,
+                      bool want_bkt = false)
 {
     if (int rc = sync_lanes(c)) return rc;
     free_lpm(t);
@@ -713,7 +744,8 @@ static int upload_lpm(cop_ctx *c, DevLpm &t, const cop_lpm_table *tab, bool want
         t.iw = iw;
     }
     int trc = 0;
-    if (want_trie && !t.m) trc = upload_trie(c, t, s, v, m);   // too large for the LDS interval form
+    if (want_bkt && !t.m) trc = upload_bkt(c, t, s, v, m);     // too large for the LDS interval form
+    else if (want_trie && !t.m) trc = upload_trie(c, t, s, v, m);
     free(s);
     free(v);
     if (trc) return trc;
@@ -776,7 +808,7 @@ int cop_set_route_lpm(cop_ctx *c, const cop_lpm_table *t)
     if (!c || !t) return -EINVAL;
     if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel is serving this context (cop_pmd_stop first)");
     const int rc = upload_lpm(c, c->lpm, t, !(c->cfg.flags & COP_CFG_LPM_FORCE_DIR24), COP_FORM_NH,
-                              (c->cfg.flags & COP_CFG_LPM_TRIE) != 0);
+                              (c->cfg.flags & COP_CFG_LPM_TRIE) != 0, (c->cfg.flags & COP_CFG_LPM_BKT) != 0);
     if (rc) (void)upload_empty_ivt(c, c->lpm);   // as cop_set_fw_table
     return rc;
 }
@@ -802,8 +834,16 @@ static int pick_mode(const cop_ctx *c, const DevLpm &t, bool enabled, bool force
     if (!enabled) return COPK_TBL_OFF;
     if (!force_dir && t.m) return COPK_TBL_IVT;
     if (!force_dir && t.tl0) return COPK_TBL_TRIE;
+    if (!force_dir && t.bidx) return COPK_TBL_BKT;
     if (t.tbl24) return COPK_TBL_DIR;
     return COPK_TBL_IVT;  // empty table (m = 4)
+}
+
+// tests: the route stage's table form a launch would use (COPK_TBL_*)
+int cop_debug_route_form(cop_ctx *c)
+{
+    if (!c) return -EINVAL;
+    return pick_mode(c, c->lpm, true, (c->cfg.flags & COP_CFG_LPM_FORCE_DIR24) != 0);
 }
 
 static void harvest_one(cop_ctx *c, Lane &L)
@@ -920,6 +960,8 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     p.lpm_tl0 = c->lpm.tl0;
     p.lpm_tnodes = c->lpm.tnodes;
     p.lpm_tleaves = c->lpm.tleaves;
+    p.lpm_bidx = c->lpm.bidx;
+    p.lpm_bpairs = c->lpm.bpairs;
     uint32_t off = 256 + c->rt_nleaf * 128;
     p.lds_fw_off = off;
     off += 2 * p.fw_m + p.fw_iw;
@@ -1502,16 +1544,17 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
 }
 
 static int pmd_hits_flush(cop_ctx *c);
+static int pmd_pause(cop_ctx *c);
+static int pmd_resume(cop_ctx *c);
 
-// Counter words [off, off + n) of the counter block into host memory `out`,
-// read — or atomically exchanged with 0 when reset — by a small kernel on
-// the telemetry stream. Safe while launches or a poll-mode kernel run: an
-// increment lands before the exchange (this read) or after it (the next),
-// none is lost or counted twice. Does not wait for submitted work.
-static int exchange_words(cop_ctx *c, size_t off, size_t n, uint64_t *out, int reset)
+// The telemetry scratch: every counter word (shards, port shards, rules),
+// so a snapshot never reallocates it (hipFree synchronises the whole
+// device: it would wait for launches in flight and for a poll-mode kernel)
+static int tele_scratch(cop_ctx *c)
 {
     HIPCHK(c, hipSetDevice(c->device));
     if (!c->tele_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->tele_stream, hipStreamNonBlocking));
+    const size_t n = RULE_OFF + c->n_rule_ctr;
     if (c->tele_words < n) {
         if (c->tele_dev) (void)hipFree(c->tele_dev);
         c->tele_dev = nullptr;
@@ -1519,15 +1562,32 @@ static int exchange_words(cop_ctx *c, size_t off, size_t n, uint64_t *out, int r
         HIPCHK(c, hipMalloc(&c->tele_dev, n * 8));
         c->tele_words = n;
     }
-    for (size_t done = 0; done < n;) {
+    return 0;
+}
+
+// Counter words [off, off + n) of the counter block into host memory `out`,
+// read — or atomically exchanged with 0 when reset — by a small kernel on
+// the telemetry stream: an increment lands before the exchange (this read)
+// or after it (the next), none is lost or counted twice. Beside one-shot
+// launches it does not wait for them. A poll-mode kernel is paused for it
+// (pmd_pause: a kernel of another stream is not guaranteed a place beside
+// it) and relaunched after.
+static int exchange_words(cop_ctx *c, size_t off, size_t n, uint64_t *out, int reset)
+{
+    if (int rc = tele_scratch(c)) return rc;
+    if (int rc = pmd_pause(c)) return rc;
+    int rc = 0;
+    for (size_t done = 0; done < n && !rc;) {
         const uint32_t k = (uint32_t)std::min<size_t>(n - done, (size_t)1 << 30);
         hipError_t e = copk_snapshot(c->counters + off + done, k, c->tele_dev + done, reset ? 1 : 0, c->tele_stream);
-        if (e != hipSuccess) return set_err(c, -EIO, "snapshot: %s", hipGetErrorString(e));
+        if (e != hipSuccess) rc = set_err(c, -EIO, "snapshot: %s", hipGetErrorString(e));
         done += k;
     }
-    HIPCHK(c, hipMemcpyAsync(out, c->tele_dev, n * 8, hipMemcpyDeviceToHost, c->tele_stream));
-    HIPCHK(c, hipStreamSynchronize(c->tele_stream));
-    return 0;
+    if (!rc && hipMemcpyAsync(out, c->tele_dev, n * 8, hipMemcpyDeviceToHost, c->tele_stream) != hipSuccess)
+        rc = set_err(c, -EIO, "snapshot copy");
+    if (!rc && hipStreamSynchronize(c->tele_stream) != hipSuccess) rc = set_err(c, -EIO, "snapshot sync");
+    const int rrc = pmd_resume(c);
+    return rc ? rc : rrc;
 }
 
 int cop_counters_read(cop_ctx *c, cop_counters *out, int reset)
@@ -1708,12 +1768,22 @@ int cop_coll_init(cop_ctx *c, const uint8_t id[COP_COLL_ID_BYTES], int rank, int
     // ($COP_COLL_PREWARM=0: off, experiments)
     const char *pw = getenv("COP_COLL_PREWARM");
     if (pw && !atoi(pw)) return 0;
-    if (c->ctr_sum_words < 1) {
+    // the reduce's buffers at their full size now (every counter word), so
+    // a reporting interval allocates nothing
+    const size_t words = RULE_OFF + c->n_rule_ctr;
+    if (c->ctr_sum_words < words) {
         if (c->ctr_sum) (void)hipFree(c->ctr_sum);
         c->ctr_sum = nullptr;
         c->ctr_sum_words = 0;
-        HIPCHK(c, hipMalloc(&c->ctr_sum, 8));
-        c->ctr_sum_words = 1;
+        HIPCHK(c, hipMalloc(&c->ctr_sum, words * 8));
+        c->ctr_sum_words = words;
+    }
+    if (c->ctr_snap_words < words) {
+        if (c->ctr_snap) (void)hipFree(c->ctr_snap);
+        c->ctr_snap = nullptr;
+        c->ctr_snap_words = 0;
+        HIPCHK(c, hipMalloc(&c->ctr_snap, words * 8));
+        c->ctr_snap_words = words;
     }
     r = g_rccl.all_reduce(c->counters, c->ctr_sum, 1, ncclUint64, ncclSum, c->comm, c->stream);
     if (r != ncclSuccess) return set_err(c, -EIO, "ncclAllReduce: %s", g_rccl.error_string(r));
@@ -1721,12 +1791,29 @@ int cop_coll_init(cop_ctx *c, const uint8_t id[COP_COLL_ID_BYTES], int rank, int
     return 0;
 }
 
+static int coll_reduce_free(cop_ctx *c, cop_counters *total, uint64_t *rule_hits, uint32_t cap, int reset);
+static int pmd_hits_sync(cop_pmd *m, uint64_t upto);
+static uint64_t pmd_refresh(cop_pmd *m, uint32_t r);
+
 int cop_coll_reduce_counters(cop_ctx *c, cop_counters *total, uint64_t *rule_hits, uint32_t cap, int reset)
 {
     if (!c || (cap && !rule_hits)) return -EINVAL;
     if (!c->comm) return set_err(c, -EINVAL, "cop_coll_init not called");
     if (int rc = sync_lanes(c)) return rc;
-    if (int rc = pmd_hits_flush(c)) return rc;
+    // the snapshot and the all-reduce run with the GPU free (pmd_pause):
+    // RCCL's kernels need room on every rank's GPU
+    if (int rc = pmd_pause(c)) return rc;
+    int rc = coll_reduce_free(c, total, rule_hits, cap, reset);
+    const int rrc = pmd_resume(c);
+    return rc ? rc : rrc;
+}
+
+// cop_coll_reduce_counters with no poll-mode kernel on the GPU
+static int coll_reduce_free(cop_ctx *c, cop_counters *total, uint64_t *rule_hits, uint32_t cap, int reset)
+{
+    if (c->pmd) {
+        if (int rc = pmd_hits_sync(c->pmd, pmd_refresh(c->pmd, 0))) return rc;
+    }
     const size_t shard_words = SHARD_WORDS;
     const size_t words = RULE_OFF + c->n_rule_ctr;
     if (c->ctr_sum_words < words) {
@@ -1797,7 +1884,9 @@ int cop_host_alloc_mapped(cop_ctx *c, size_t bytes, void **hptr, void **dptr)
 {
     if (!c || !hptr || !dptr) return -EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocMapped));
+    // coherent (fine-grained): a poll-mode kernel never ends, so its stores
+    // must reach host memory without the kernel-end write-back of the L2
+    HIPCHK(c, hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocMapped | hipHostMallocCoherent));
     hipError_t e = hipHostGetDevicePointer(dptr, *hptr, 0);
     if (e != hipSuccess) {
         (void)hipHostFree(*hptr);
@@ -1904,6 +1993,8 @@ struct cop_pmd {
     size_t dev_bytes = 0;
     uint32_t n_rings = 1, n_slots = 0, tpb = 0, per_cu = 0, ring_n = 0;
     std::atomic<uint32_t> launches{0};
+    uint32_t pauses = 0;                    // pmd_pause calls that stopped a running kernel
+    bool was_live = false;                  // pmd_pause found it running (pmd_resume relaunches)
     bool live = false;                      // a launch may still be running
     std::mutex mu;                          // relaunch after an idle exit, from any ring's thread
     PmdRing ring[COPK_PMD_MAX_RINGS];
@@ -1976,14 +2067,14 @@ static int pmd_join(cop_pmd *m, double timeout_s)
         if (e != hipErrorNotReady) return set_err(m->c, -EIO, "pmd: %s", hipGetErrorString(e));
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
             return set_err(m->c, -ETIMEDOUT, "pmd: kernel did not leave within %.0f s", timeout_s);
-        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
     m->live = false;
     return 0;
 }
 
 // advance ring r's completed count over its completion words (the ring's thread)
-static uint64_t pmd_refresh(cop_pmd *m, uint32_t r = 0)
+static uint64_t pmd_refresh(cop_pmd *m, uint32_t r)
 {
     PmdRing &g = m->ring[r];
     const uint64_t posted = g.posted.load(std::memory_order_relaxed);
@@ -2026,11 +2117,16 @@ static int pmd_hits_sync(cop_pmd *m, uint64_t upto)
     return 0;
 }
 
+// count every completed batch's binned hits, with the GPU free (pmd_pause)
 static int pmd_hits_flush(cop_ctx *c)
 {
     cop_pmd *m = c->pmd;
     if (!m || !m->bins) return 0;
-    return pmd_hits_sync(m, pmd_refresh(m, 0));
+    if (m->count_synced >= pmd_refresh(m, 0) && m->ring[0].posted.load() == m->count_synced) return 0;
+    if (int rc = pmd_pause(c)) return rc;
+    int rc = pmd_hits_sync(m, pmd_refresh(m, 0));
+    const int rrc = pmd_resume(c);
+    return rc ? rc : rrc;
 }
 
 // every worker must be resident at once (static tile order): all of the
@@ -2052,6 +2148,7 @@ static void pmd_size(cop_pmd *m)
     m->P.poll_backoff = 3;
     m->P.stepwise = getenv("COP_PMD_STEPWISE") && !atoi(getenv("COP_PMD_STEPWISE")) ? 0u : 1u;
     if (const char *e = getenv("COP_PMD_BACKOFF")) m->P.poll_backoff = std::min(64u, (uint32_t)atoi(e));
+    m->P.prefetch = getenv("COP_PMD_PREFETCH") && atoi(getenv("COP_PMD_PREFETCH")) ? 1u : 0u;
 }
 
 // wait for the launch's census: 0 = every worker resident, 1 = aborted
@@ -2065,7 +2162,7 @@ static int pmd_census(cop_pmd *m)
         if (m->h_state[0] != COPK_PMD_RUNNING) return set_err(m->c, -EIO, "pmd: left during the census");
         if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 5.0)
             return set_err(m->c, -ETIMEDOUT, "pmd: no census after 5 s");
-        std::this_thread::sleep_for(std::chrono::microseconds(20));
+        std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
 }
 
@@ -2085,11 +2182,7 @@ static int pmd_prewarm(cop_pmd *m)
         if (e != hipSuccess) return set_err(c, -EIO, "pmd prewarm: %s", hipGetErrorString(e));
         HIPCHK(c, hipStreamSynchronize(m->hs));
     }
-    if (!c->tele_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->tele_stream, hipStreamNonBlocking));
-    if (!c->tele_dev) {
-        HIPCHK(c, hipMalloc(&c->tele_dev, 8));
-        c->tele_words = 1;
-    }
+    if (int rc = tele_scratch(c)) return rc;
     for (hipStream_t s : {c->tele_stream, c->stream}) {
         hipError_t e = copk_snapshot(c->counters, 1, c->tele_dev, 0, s);
         if (e != hipSuccess) return set_err(c, -EIO, "pmd prewarm: %s", hipGetErrorString(e));
@@ -2126,10 +2219,49 @@ static int pmd_revive(cop_pmd *m)
     std::lock_guard<std::mutex> lk(m->mu);
     const uint32_t why = m->h_state[0];
     if (why == COPK_PMD_RUNNING) return 0;   // another ring's thread relaunched it
-    if (why != COPK_PMD_IDLE) return set_err(m->c, -EIO, "pmd kernel left (%s)", why == COPK_PMD_ABORT ?
-                                             "abort: workers not co-resident, or a look-back timed out" : "stopped");
+    if (why != COPK_PMD_IDLE && why != COPK_PMD_PAUSED)
+        return set_err(m->c, -EIO, "pmd kernel left (%s)", why == COPK_PMD_ABORT ?
+                       "abort: workers not co-resident, or a look-back timed out" : "stopped");
     if (int rc = pmd_join(m, 10.0)) return rc;
     return pmd_launch_resident(m);
+}
+
+// Make the GPU free for kernels the host must see finish while a poll-mode
+// kernel serves the context: the binned hit count and the RCCL all-reduce
+// of the counters. The poll-mode kernel holds every workgroup slot it may
+// use, and a kernel of another stream beside it is not guaranteed to run
+// (round 3's config-5 record: cop_hit_count waited 1 s for the idle exit;
+// DESIGN.md §14.1). So the host asks it to leave (h_stop = 2: it closes its
+// gates and finishes every batch below them, as an idle exit does), waits
+// until it has left, runs the side work, and relaunches it (pmd_resume).
+// Holds the relaunch lock in between: a ring's post or wait meanwhile
+// blocks in pmd_revive until the relaunch.
+static int pmd_pause(cop_ctx *c)
+{
+    cop_pmd *m = c->pmd;
+    if (!m) return 0;
+    m->mu.lock();
+    m->was_live = m->live && m->h_state[0] == COPK_PMD_RUNNING;
+    if (m->was_live) {
+        *m->h_stop = 2u;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+    }
+    const int rc = pmd_join(m, 10.0);
+    if (rc) m->mu.unlock();
+    else m->pauses += m->was_live ? 1u : 0u;
+    return rc;
+}
+
+// relaunch after pmd_pause (only if it was running then: a kernel that had
+// left idle is relaunched by the next post, as always)
+static int pmd_resume(cop_ctx *c)
+{
+    cop_pmd *m = c->pmd;
+    if (!m) return 0;
+    int rc = 0;
+    if (m->was_live && !m->live && m->h_state[0] == COPK_PMD_PAUSED) rc = pmd_launch_resident(m);
+    m->mu.unlock();
+    return rc;
 }
 
 // ring geometry every ring of one kernel shares (the kernel is instantiated
@@ -2395,7 +2527,7 @@ int cop_pmd_wait_ring(cop_pmd *m, uint32_t ring, uint64_t seq)
                            (unsigned long long)g.completed.load());
     }
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    return ring == 0 ? pmd_hits_launch(m) : 0;
+    return 0;
 }
 
 int cop_pmd_wait(cop_pmd *m, uint64_t seq) { return cop_pmd_wait_ring(m, 0, seq); }
@@ -2412,8 +2544,13 @@ static int pmd_post(cop_pmd *m, uint32_t r, uint32_t count, uint32_t n_each)
     const uint64_t need = posted + count;
     if (need - g.completed.load(std::memory_order_relaxed) > m->n_slots)
         if (int rc = cop_pmd_wait_ring(m, r, need - m->n_slots)) return rc;
-    if (r == 0 && need > m->n_slots)   // the reused slots' binned hits are counted first
-        if (int rc = pmd_hits_sync(m, need - m->n_slots)) return rc;
+    if (r == 0 && m->bins && need > m->n_slots && m->count_synced < need - m->n_slots) {
+        // the reused slots' binned hits are counted first, with the GPU free
+        if (int rc = pmd_pause(m->c)) return rc;
+        int rc = pmd_hits_sync(m, need - m->n_slots);
+        const int rrc = pmd_resume(m->c);
+        if (rc || rrc) return rc ? rc : rrc;
+    }
     if (int rc = pmd_revive(m)) return rc;
     if (m->h_n)
         for (uint64_t b = posted; b < need; b++)
@@ -2487,11 +2624,11 @@ int cop_pmd_stop(cop_pmd *m)
     cop_ctx *c = m->c;
     int rc = 0;
     for (uint32_t r = 0; r < m->n_rings && !rc; r++) rc = cop_pmd_wait_ring(m, r, m->ring[r].posted.load());
-    if (!rc) rc = pmd_hits_sync(m, m->ring[0].completed.load());
     *m->h_stop = 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     const int jrc = pmd_join(m, 10.0);
     if (!rc) rc = jrc;
+    if (!rc) rc = pmd_hits_sync(m, m->ring[0].completed.load());   // the GPU is free now
     if (m->hs) (void)hipStreamSynchronize(m->hs);
     if (!jrc) {
         if (m->s) (void)hipStreamDestroy(m->s);

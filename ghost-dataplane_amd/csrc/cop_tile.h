@@ -188,7 +188,8 @@ __device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &
 template <int FW, int LPM, int LAY, bool EXT>
 constexpr bool steps_ok()
 {
-    return !EXT && LAY == COPK_LAY_COALESCED && FW != COPK_TBL_DIR && LPM != COPK_TBL_DIR && LPM != COPK_TBL_TRIE;
+    return !EXT && LAY == COPK_LAY_COALESCED && FW != COPK_TBL_DIR && LPM != COPK_TBL_DIR && LPM != COPK_TBL_TRIE &&
+           LPM != COPK_TBL_BKT;
 }
 
 // One tile of the poll-mode kernel, step by step (tile_body does the same
@@ -208,9 +209,11 @@ constexpr bool steps_ok()
 #ifndef COPK_PMD_WIN
 #define COPK_PMD_WIN 4
 #endif
-template <int FW, int LPM, int PPT, bool WT>
+// pf: called once the tile's first loads are issued (the poll-mode kernel's
+// L2 prefetch of its next tile, which then queues behind this tile's loads)
+template <int FW, int LPM, int PPT, bool WT, typename Pf>
 __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
-                                           int tid, int lane, int wave)
+                                           int tid, int lane, int wave, Pf pf)
 {
     static_assert(COPK_SEG == BLOCK, "one segment per tile step");
     const Tables &tb = lc.tb;
@@ -225,6 +228,7 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
     u32x4 v[W][3];
 #pragma unroll
     for (int k = 0; k < W; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
+    pf();
     Counts tot;
     uint32_t *r = (uint32_t *)B.results;
     const int i2 = lane & 31;
@@ -235,15 +239,15 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
         if (k + W < PPT) load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W]);
         const uint32_t pk0 = base + k * BLOCK;
         const bool valid[1] = {pk0 + tid < B.n && B.n != 0};
-        uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], src[1], dst[1], ct = 0, cn = 0;
+        uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], lpe2[1], src[1], dst[1], ct = 0, cn = 0;
         if (COPK_XP & 1) {
             verdict[0] = (w3[0] ^ w6[0] ^ w7[0] ^ w8[0]) & 1u;
             port[0] = w7[0] & 3u;
             flags[0] = 0;
             rnh[0] = w8[0];
         } else {
-            pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe);
-            pass2<FW, LPM, 1>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, ct, cn);
+            pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2);
+            pass2<FW, LPM, 1>(p, w3, src, dst, valid, fwe, lpe, lpe2, verdict, flags, rnh, ct, cn);
         }
         const Counts c = wave_counts<FW, 1>(valid, verdict, flags);
         tot.total += c.total;
@@ -384,8 +388,8 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
     if (sync_tables) __syncthreads();   // LDS-DMA table staging has landed
 
     // ---- pass 1 (parse, route, LDS searches, tbl24 loads issued) ----
-    uint32_t verdict[PPT], port[PPT], flags[PPT], rnh[PPT], fwe[PPT], lpe[PPT], src[PPT], dst[PPT];
-    pass1<FW, LPM, PPT>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe);
+    uint32_t verdict[PPT], port[PPT], flags[PPT], rnh[PPT], fwe[PPT], lpe[PPT], lpe2[PPT], src[PPT], dst[PPT];
+    pass1<FW, LPM, PPT>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2);
     if (o.dbg & 8u) {
         uint32_t x = 0;
 #pragma unroll
@@ -396,7 +400,7 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
 
     // ---- pass 2 (tbl8 step) and the verdicts ----
     Counts cn;
-    pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, verdict, flags, rnh, cn.total, cn.notv4);
+    pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, lpe2, verdict, flags, rnh, cn.total, cn.notv4);
     const bool bins = EXT && FW != COPK_TBL_OFF && p.hit_region != nullptr;
     // segmented lists with no optional feature: the lean epilogue (counters
     // from ballots, folded into the list's barriers)

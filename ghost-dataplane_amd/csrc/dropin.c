@@ -58,6 +58,12 @@ static __thread struct {
     uint32_t cap;
 } tl_buf;
 
+/* forward_batch's list of the mbufs to free (per thread) */
+static __thread struct {
+    void **drop;
+    uint32_t cap;
+} tl_fwd;
+
 /* Diagnostic per-op host time of this thread's ring loop ($COP_HOST_PROF=1,
  * cop_debug_dropin_prof): ns in drain (dequeue + mbuf data addresses),
  * batch (cop_process_host_stages: gather, launch, wait, copy-out; or the
@@ -224,6 +230,9 @@ int coprocessor_teardown(void)
     free(tl_buf.data);
     free(tl_buf.res);
     memset(&tl_buf, 0, sizeof(tl_buf));
+    free(tl_fwd.drop);
+    tl_fwd.drop = NULL;
+    tl_fwd.cap = 0;
     return rc;
 }
 
@@ -262,27 +271,35 @@ int process_packet(struct rte_mbuf *pkt)
 
 /* forward in arrival order through a PKT_BURST_SZ tx buffer flushed with
  * an all-or-nothing bulk enqueue (enqueue_nf_tx / flush_nf_tx_queue,
- * switch.c:240-280,329-351); drops are freed (switch.c:469). */
+ * switch.c:240-280,329-351); drops are freed (switch.c:469). The verdicts
+ * are split without branches (a forward/drop branch mispredicts on every
+ * third packet): the forwarded mbufs go to the tx bursts in order, the
+ * dropped ones to a list freed after. */
 static void forward_batch(cop_ring *tx, void *const *objs, const cop_result *res, uint32_t n, cop_free_fn free_fn,
                           void *free_arg, cop_nf_stats *stats)
 {
-    void *txb[COP_PKT_BURST_SZ];
-    uint32_t cnt = 0;
-    for (uint32_t i = 0; i <= n; i++) {
-        int flush = (i == n) ? cnt > 0 : 0;
-        if (i < n) {
-            struct rte_mbuf *m = (struct rte_mbuf *)objs[i];
-            if (res[i].verdict == COP_FORWARD) {
-                txb[cnt++] = m;
-                flush = cnt == COP_PKT_BURST_SZ;
-            } else if (free_fn) {
-                free_fn(m, free_arg);
-            }
+    if (tl_fwd.cap < n) {
+        void **d = (void **)realloc(tl_fwd.drop, (n < 1024 ? 1024 : n) * sizeof(void *));
+        if (!d) {   /* no scratch: free nothing lost, forward nothing (counted) */
+            drop_all(objs, n, free_fn, free_arg, stats);
+            return;
         }
-        if (flush) {
+        tl_fwd.drop = d;
+        tl_fwd.cap = n < 1024 ? 1024 : n;
+    }
+    void **drop = tl_fwd.drop;
+    void *txb[COP_PKT_BURST_SZ + 1];
+    uint32_t cnt = 0, nd = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        void *m = objs[i];
+        const uint32_t f = res[i].verdict == COP_FORWARD;
+        txb[cnt] = m;
+        drop[nd] = m;
+        cnt += f;
+        nd += 1u - f;
+        if (cnt == COP_PKT_BURST_SZ || (i + 1 == n && cnt)) {
             uint32_t sent = cop_ring_enqueue_bulk(tx, txb, cnt, NULL);
-            if (sent < cnt && free_fn)
-                for (uint32_t k = sent; k < cnt; k++) free_fn((struct rte_mbuf *)txb[k], free_arg);
+            for (uint32_t k = sent; k < cnt; k++) drop[nd++] = txb[k];   /* a burst that does not fit */
             if (stats) {
                 stats->tx_packets += sent;
                 stats->tx_dropped += cnt - sent;
@@ -290,6 +307,8 @@ static void forward_batch(cop_ring *tx, void *const *objs, const cop_result *res
             cnt = 0;
         }
     }
+    if (free_fn)
+        for (uint32_t k = 0; k < nd; k++) free_fn((struct rte_mbuf *)drop[k], free_arg);
 }
 
 /* dequeue up to max_pkts from rx (switch.c:463 dequeues PKT_BURST_SZ per

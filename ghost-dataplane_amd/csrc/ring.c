@@ -69,6 +69,11 @@ uint32_t cop_ring_enqueue_bulk(cop_ring *r, void *const *objs, uint32_t n, uint3
         if (free_space) *free_space = free_entries;
         return 0;
     }
+    /* the slots two bursts ahead were last read by the consumer's core: ask
+     * for them in exclusive state now (prefetch for write), so the stores
+     * of a later call do not each wait for a line transfer (ring loop
+     * profile: 16 ns/pkt in the tx enqueue without it) */
+    for (uint32_t i = 0; i < n; i += 8) __builtin_prefetch(&r->slots[(head + 2 * n + i) & r->mask], 1, 3);
     for (uint32_t i = 0; i < n; i++) r->slots[(head + i) & r->mask] = objs[i];
     atomic_store_explicit(&r->prod, head + n, memory_order_release);
     if (free_space) *free_space = free_entries - n;

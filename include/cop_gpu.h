@@ -72,9 +72,9 @@ extern "C" {
  *     (no NF stage), as process_packet does without ENABLE_FW_NF
  *     (coprocessor.c:59-64). Define COP_DROPIN_NO_NF for that chain alone.
  * The library is built once, so the caller's macros reach it through
- * coprocessor_setup(), which this header turns into
- * cop_coprocessor_setup_stages(COP_DROPIN_STAGES) in the caller's build
- * (cop_set_dropin_stages sets the same at run time, e.g. from an FFI). */
+ * coprocessor_setup, which this header makes an alias of
+ * cop_coprocessor_setup_fw or cop_coprocessor_setup_no_nf in the caller's
+ * build (cop_set_dropin_stages sets the same at run time, e.g. from an FFI). */
 #if defined(DISABLE_NF) || defined(COP_DROPIN_NO_NF)
 #define COP_DROPIN_STAGES 0u
 #else
@@ -235,6 +235,12 @@ typedef struct cop_ctx cop_ctx;
  * need no cross-workgroup prefix. Not combinable with DEMUX_PORTS. */
 #define COP_CFG_SEG_LISTS       0x80u
 #define COP_SEG_PKTS            256u
+/* Route tables too large for LDS: look them up in the bucketed interval form
+ * in global memory (a few MiB that stay in L2 / the Infinity Cache): the
+ * bucket of the address's top bits gives the first candidate interval, one
+ * 16-byte load of two (start, value) pairs decides almost every lookup.
+ * Results are identical; takes precedence over COP_CFG_LPM_TRIE. */
+#define COP_CFG_LPM_BKT         0x100u
 #define COP_MAX_DEMUX_PORTS     8
 
 typedef struct cop_config {
@@ -381,13 +387,22 @@ int  cop_host_batch_wait(cop_ctx *ctx, uint32_t slot, const cop_result **results
  * exactly those of cop_submit_ring. No launch per post: no launch latency,
  * no grid ramp, tables staged into LDS once.
  * While it runs, the context's tables cannot change (-EBUSY) and it holds
- * most workgroup slots of the GPU (other launches on the context still run,
- * beside it). Counters stay readable: cop_counters_read /
- * cop_counters_snapshot / cop_rule_counters_read see every completed batch
- * (a batch's counter adds land before its completion), and their reset is
- * an atomic read-and-zero, so nothing is lost or counted twice while
- * batches run. One per context. The kernel leaves by itself after 1 s
- * without a post ($COP_PMD_IDLE_MS) and is relaunched by the next post. */
+ * every worker slot it could get: another kernel is NOT guaranteed to run
+ * beside it. Counters stay readable: cop_counters_read /
+ * cop_counters_snapshot / cop_rule_counters_read / cop_coll_reduce_counters
+ * see every completed batch (a batch's counter adds land before its
+ * completion), and their reset is an atomic read-and-zero, so nothing is
+ * lost or counted twice while batches run. Those that need a kernel of
+ * their own (the rule-hit count, the snapshot, the RCCL all-reduce) PAUSE
+ * the poll-mode kernel: it finishes every batch posted so far and leaves,
+ * the side work runs, and it is relaunched (microseconds, not a wait for
+ * an idle exit). Posts during a pause wait for the relaunch. One per
+ * context. The kernel leaves by itself after 1 s without a post
+ * ($COP_PMD_IDLE_MS) and is relaunched by the next post.
+ * A ring whose pkts / results / lists live in mapped host memory must be
+ * allocated coherent (cop_host_alloc_mapped does): a persistent kernel has
+ * no kernel-end cache writeback, so its stores to non-coherent host pages
+ * can stay in the GPU's L2. */
 typedef struct cop_pmd cop_pmd;
 int cop_pmd_start(cop_ctx *ctx, const cop_batch_ring *ring, cop_pmd **out);
 /* Post the next `count` batches (<= n_slots): sequence numbers posted ..
@@ -408,7 +423,7 @@ typedef struct cop_pmd_info_t {
     uint32_t tiles_per_batch;
     uint32_t packets_per_tile;
     uint32_t launches;         /* 1 + relaunches after idle exits */
-    uint32_t state;            /* 0 running, 1 stopped, 2 left idle, 3 aborted */
+    uint32_t state;            /* 0 running, 1 stopped, 2 left idle, 3 aborted, 4 paused */
     uint64_t posted, completed; /* summed over the rings */
 } cop_pmd_info_t;
 int cop_pmd_info(const cop_pmd *pmd, cop_pmd_info_t *out);
@@ -523,6 +538,10 @@ int  cop_dev_alloc(cop_ctx *ctx, size_t bytes, void **dptr);
 int  cop_dev_free(cop_ctx *ctx, void *dptr);
 int  cop_host_alloc_pinned(cop_ctx *ctx, size_t bytes, void **hptr);
 int  cop_host_free_pinned(cop_ctx *ctx, void *hptr);
+/* Pinned host memory the device reads and writes coherently (mapped into
+ * the device's address space; *dptr is the device's pointer to it): rings a
+ * poll-mode kernel serves from host memory. Free with cop_host_free_pinned. */
+int  cop_host_alloc_mapped(cop_ctx *ctx, size_t bytes, void **hptr, void **dptr);
 int  cop_memcpy_h2d(cop_ctx *ctx, void *dst, const void *src, size_t bytes);
 int  cop_memcpy_d2h(cop_ctx *ctx, void *dst, const void *src, size_t bytes);
 int  cop_memcpy_d2d(cop_ctx *ctx, void *dst, const void *src, size_t bytes);

@@ -64,7 +64,8 @@ def test_fw_dir24_forced(gpu_ctx_factory):
     assert_parity(rg, fg, ro, fo)
 
 
-FORMS = {"dir": 0, "trie": cg.CFG_LPM_TRIE}   # the 100k route table: DIR-24-8 or the multibit trie
+# the 100k route table: DIR-24-8, the multibit trie or the bucketed intervals
+FORMS = {"dir": 0, "trie": cg.CFG_LPM_TRIE, "bkt": cg.CFG_LPM_BKT}
 
 
 @pytest.mark.parametrize("form", list(FORMS))
@@ -72,6 +73,7 @@ def test_fw_lpm_100k(gpu_ctx_factory, form):
     rules = fw1k()
     routes = routes100k()
     ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=S | F | L, flags=FORMS[form])
+    assert ctx.route_form() == form
     n = 65536
     pk = cg.gen_trace(0x5EED0003, n, rules, routes)
     fwo, rto = oracle_tables(rules, routes)

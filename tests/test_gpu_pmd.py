@@ -160,13 +160,13 @@ def test_pmd_layouts(gpu_ctx_factory, layout):
     check(*rg.read(), ro, fos, B, P)
 
 
-@pytest.mark.parametrize("form", ["dir", "trie"])
+@pytest.mark.parametrize("form", ["dir", "trie", "bkt"])
 def test_pmd_imix(gpu_ctx_factory, form):
     """IMIX slab + u32 offsets per slot; the 20k-route table (beyond LDS) as
     DIR-24-8 or in the multibit-trie form."""
     rules = fw1k()
     rts = routes(20000)
-    ctx = gpu_ctx_factory(stages=S | F | L, flags=cg.CFG_LPM_TRIE if form == "trie" else 0)
+    ctx = gpu_ctx_factory(stages=S | F | L, flags={"dir": 0, "trie": cg.CFG_LPM_TRIE, "bkt": cg.CFG_LPM_BKT}[form])
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     ctx.set_route_lpm(cg.LpmTable(rts, 1 << 20, 1 << 16, False))
     B, P = 20000, 3
@@ -194,7 +194,7 @@ def test_pmd_imix(gpu_ctx_factory, form):
         assert int(cnt[s]) == len(f1) and np.array_equal(fwd[s * B:s * B + len(f1)], f1)
 
 
-@pytest.mark.parametrize("form", ["dir", "trie"])
+@pytest.mark.parametrize("form", ["dir", "trie", "bkt"])
 def test_pmd_dir24_rule_counters(gpu_ctx_factory, form):
     """FW stage DIR-24-8 in HBM, the route stage DIR-24-8 or trie, per-rule
     hit counters (the EXT kernel): counters equal the oracle's hits over
@@ -202,7 +202,7 @@ def test_pmd_dir24_rule_counters(gpu_ctx_factory, form):
     rules = fw1k()
     rts = routes()
     ctx = gpu_ctx_factory(stages=S | F | L, flags=cg.CFG_FW_FORCE_DIR24 | cg.CFG_RULE_COUNTERS
-                          | (cg.CFG_LPM_TRIE if form == "trie" else 0))
+                          | {"dir": 0, "trie": cg.CFG_LPM_TRIE, "bkt": cg.CFG_LPM_BKT}[form])
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
     ctx.set_route_lpm(cg.LpmTable(rts, 1 << 20, 1 << 16, False))
     B, P = 65536, 6
@@ -283,3 +283,45 @@ def test_pmd_idle_exit_relaunch_and_restart(gpu_ctx_factory, monkeypatch):
         m2.post(P)
         m2.wait()
     check(*rg.read(), ro, fos, B, P)
+
+
+def test_pmd_counter_reduce_while_serving(gpu_ctx_factory, monkeypatch):
+    """The config-5 stall: with a poll-mode kernel live (a long
+    idle spell, so it never leaves on its own) and 100k-rule per-rule
+    counters, every RCCL counter reduce and every rule-counter read returns
+    in well under 50 ms with exact sums. Side work pauses the kernel
+    (cop_runtime.cpp pmd_pause / pmd_resume) instead of waiting for it to go
+    idle — a side kernel is not guaranteed to run beside it."""
+    monkeypatch.setenv("COP_PMD_IDLE_MS", "20000")
+    fw_rules = cg.gen_rules(0x5EED1077, 100000, cg.GEN_FW, 0)
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_RULE_COUNTERS)
+    ctx.set_fw_table(cg.LpmTable(fw_rules, 100000, 1 << 20, False))
+    ctx.coll_init(cg.coll_unique_id(), 0, 1)
+    ofw = orc.OracleLpm(100000, 1 << 20, rules_only=True)
+    ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=False)
+    B, P = 65536, 4
+    pk = cg.gen_trace(0x5EED0B70, B * P, fw_rules)
+    hits = np.zeros(ofw.n_rules, np.uint64)
+    ro, _, co = orc.process(pk, B * P, stages=S | F, fw=ofw, rule_hits=hits)
+    assert hits.sum() > B
+    rg = Ring(ctx, pk, B, P)
+    ctx.counters(reset=True)
+    times = []
+    with ctx.pmd_start(rg.ring) as m:
+        for rnd in range(5):
+            m.post(P)
+            m.wait()
+            t0 = time.perf_counter()
+            got = ctx.rule_counters()
+            t1 = time.perf_counter()
+            tot, red = ctx.coll_reduce_counters(reset=True)
+            t2 = time.perf_counter()
+            times.append((round((t1 - t0) * 1e3, 3), round((t2 - t1) * 1e3, 3)))
+            assert np.array_equal(got, hits), f"round {rnd}: rule counters"
+            assert np.array_equal(red, hits), f"round {rnd}: reduced rule counters"
+            for k in co:
+                assert tot[k] == co[k], (rnd, k, tot[k], co[k])
+        res, _, _ = rg.read()
+        assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
+        assert m.info()["launches"] >= 1
+    assert all(a < 50 and b < 50 for a, b in times), times

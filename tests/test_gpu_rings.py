@@ -164,3 +164,37 @@ def test_rings_reject_mismatched_geometry(gpu_ctx_factory):
         ctx.pmd_start([a.ring, b.ring])
     with pytest.raises(cg.CopError):
         ctx.pmd_start([a.ring] * 9)
+
+
+@pytest.mark.parametrize("stages", [F, S | F])
+def test_hdr16_rings_variable_n(gpu_ctx_factory, stages):
+    """The drop-in's kernel shape through the batch-ring API: two rings of
+    packed 16-byte header records (COP_HDR16_STRIDE), variable-size batches,
+    no forward lists, the firewall alone (the drop-in's NF chain) or P + FW:
+    records equal the oracle's for the first n packets of every batch."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=stages)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    fw, _ = oracle_tables(rules)
+    B, P, R = 4096, 4, 2
+    pks = [cg.gen_trace(0x5EED7400 + r, B * P, rules) for r in range(R)]
+    bufs, rings = [], []
+    for r in range(R):
+        hdr = cg.pack_headers_np(pks[r], B * P)
+        dp = ctx.alloc(hdr.nbytes)
+        dp.upload(hdr)
+        dr = ctx.alloc(B * P * 8)
+        dr.fill(0xEE)
+        bufs.append((dp, dr))
+        rings.append(cg.make_ring(dp, P, B, dr, B * cg.HDR16_STRIDE, stride=cg.HDR16_STRIDE))
+    sizes = [4096, 1, 2500, 1024, 1025, 77, 4095, 3000]
+    with ctx.pmd_start(rings, cg.PMD_VARIABLE_N) as m:
+        for i, n in enumerate(sizes):
+            for r in range(R):
+                m.post_batch(r, n)
+            for r in range(R):
+                m.wait_ring(r)
+                s_ = i % P
+                res = bufs[r][1].download(cg.RESULT_DT, B * P)[s_ * B:s_ * B + n]
+                ro, _, _ = orc.process(pks[r][s_ * B * 64:(s_ * B + n) * 64], n, stages=stages, fw=fw)
+                assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"ring {r} batch {i} (n={n})"

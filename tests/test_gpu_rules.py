@@ -101,7 +101,7 @@ def test_rule_counters_off_by_default(gpu_ctx_factory):
         ctx.rule_counters()
 
 
-@pytest.mark.parametrize("form", ["dir", "trie"])
+@pytest.mark.parametrize("form", ["dir", "trie", "bkt"])
 def test_config5_scale_1m_rules_1m_prefixes(gpu_ctx_factory, form):
     """BASELINE configs[4] tables at full size, one 256k batch, full parity;
     the 1M-prefix route table as DIR-24-8 or as the multibit trie."""
@@ -111,7 +111,7 @@ def test_config5_scale_1m_rules_1m_prefixes(gpu_ctx_factory, form):
     fwt = cg.LpmTable(fw_rules, 1000000, 1 << 20, False)
     rtt = cg.LpmTable(routes, 1000000, 1 << 20, False)
     ctx = gpu_ctx_factory(stages=S | F | L, max_batch=262144,
-                          flags=cg.CFG_RULE_COUNTERS | (cg.CFG_LPM_TRIE if form == "trie" else 0))
+                          flags=cg.CFG_RULE_COUNTERS | {"dir": 0, "trie": cg.CFG_LPM_TRIE, "bkt": cg.CFG_LPM_BKT}[form])
     ctx.set_fw_table(fwt)
     ctx.set_route_lpm(rtt)
     ofw = orc.OracleLpm(1000000, 1 << 20, rules_only=True)

@@ -6,7 +6,8 @@ must stay bit-identical with thousands of tbl8 groups, a /16 holding 6000
 host routes, /1 prefixes and the two ends of the address space — with the
 default mode selection, with FORCE_DIR24 set explicitly, with the
 tbl8 groups in their packed run-block form ($COP_TBL8=packed), and with the
-route stage in its multibit-trie form (CFG_LPM_TRIE).
+route stage in its multibit-trie form (CFG_LPM_TRIE) and in its bucketed
+interval form (CFG_LPM_BKT).
 """
 import numpy as np
 import pytest
@@ -19,9 +20,10 @@ pytestmark = pytest.mark.gpu
 
 S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
 DIR = cg.CFG_FW_FORCE_DIR24 | cg.CFG_LPM_FORCE_DIR24
-# trie: the route stage in its multibit-trie form (LDS top level + L2 nodes)
+# trie: the route stage in its multibit-trie form (LDS top level + L2 nodes);
+# bkt: in its bucketed interval form (index + (start, value) pairs in L2)
 MODES = {"auto": (0, "plain"), "forced": (DIR, "plain"), "packed": (DIR, "packed"),
-         "trie": (cg.CFG_LPM_TRIE, "plain")}
+         "trie": (cg.CFG_LPM_TRIE, "plain"), "bkt": (cg.CFG_LPM_BKT, "plain")}
 
 
 def dense_routes():
@@ -52,6 +54,7 @@ def test_large_fw_and_routes(gpu_ctx_factory, mode, monkeypatch):
     ctx = gpu_ctx_factory(stages=S | F | L, flags=MODES[mode][0] | cg.CFG_RULE_COUNTERS)
     ctx.set_fw_table(fwt)
     ctx.set_route_lpm(rtt)
+    assert ctx.route_form() == {"trie": "trie", "bkt": "bkt"}.get(mode, "dir")
     ofw = orc.OracleLpm(20000, 1 << 16)
     ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=False)
     ort = orc.OracleLpm(1 << 20, 1 << 16)
@@ -87,6 +90,7 @@ def test_large_table_all_addresses_of_a_dense_chunk(gpu_ctx_factory, mode, monke
     rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
     ctx = gpu_ctx_factory(stages=S | L, flags=MODES[mode][0])
     ctx.set_route_lpm(rtt)
+    assert ctx.route_form() == {"trie": "trie", "bkt": "bkt"}.get(mode, "dir")
     ort = orc.OracleLpm(1 << 20, 1 << 16)
     ort.setup(routes["ip"], routes["depth"], routes["next_hop"], stop_at_error=False)
     n = 65536

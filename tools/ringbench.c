@@ -28,6 +28,7 @@
  */
 #define _GNU_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -60,7 +61,7 @@ typedef struct loop {
     uint8_t *data;
     uint64_t n_total, processed, polls, freed;
     uint64_t prof[7], hprof[6];   /* $COP_HOST_PROF=1: per-op host ns (cop_debug_*_prof) */
-    _Atomic uint64_t n_tx;
+    _Alignas(64) _Atomic uint64_t n_tx;   /* the tx thread's: its own line */
     atomic_int done, ready;
     int rc;
     uint32_t id;
@@ -73,6 +74,8 @@ static cop_pmd_host *g_ph;
 static char g_rules[64];
 static atomic_int g_go;
 
+static void pin_to(int k);
+
 static void free_mbuf(struct rte_mbuf *m, void *arg)
 {
     (void)m;
@@ -82,6 +85,7 @@ static void free_mbuf(struct rte_mbuf *m, void *arg)
 static void *fastpath(void *arg)
 {
     loop *L = arg;
+    pin_to(3 * (int)L->id);
     void *burst[COP_PKT_BURST_SZ];
     while (!atomic_load(&g_go)) {
     }
@@ -96,6 +100,7 @@ static void *fastpath(void *arg)
 static void *txdrain(void *arg)
 {
     loop *L = arg;
+    pin_to(3 * (int)L->id + 2);
     void *burst[COP_PKT_BURST_SZ];
     for (;;) {
         uint32_t got = cop_ring_dequeue_burst(L->tx, burst, COP_PKT_BURST_SZ, NULL);
@@ -120,6 +125,7 @@ static int poll_once(cop_ctx *ctx, loop *L, cop_nf_stats *st)
 static void *coprocessor(void *arg)
 {
     loop *L = arg;
+    pin_to(3 * (int)L->id + 1);
     if (!g_pmd && coprocessor_setup() != 0) {
         L->rc = 4;
         atomic_store(&L->done, 1);
@@ -166,6 +172,29 @@ static void *coprocessor(void *arg)
         coprocessor_teardown();
     }
     return NULL;
+}
+
+/* Pin the calling thread to the k-th CPU this process may use, counting
+ * from the 5th (the first few also serve interrupts and the main thread):
+ * DPDK lcores are pinned, and a loop's three threads on adjacent cores keep
+ * the ring transfers between them inside one CCD ($RINGBENCH_PIN=0: off). */
+static void pin_to(int k)
+{
+    const char *e = getenv("RINGBENCH_PIN");
+    if (e && !atoi(e)) return;
+    cpu_set_t all;
+    if (sched_getaffinity(0, sizeof(all), &all)) return;
+    int seen = 0;
+    for (int c = 0; c < CPU_SETSIZE; c++) {
+        if (!CPU_ISSET(c, &all)) continue;
+        if (seen++ == k + 4) {
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(c, &one);
+            pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+            return;
+        }
+    }
 }
 
 static double now(void)
