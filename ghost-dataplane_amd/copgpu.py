@@ -649,6 +649,7 @@ class Context:
 
 
 PMD_VARIABLE_N = 1
+PMD_SYS_ACQUIRE = 2
 
 
 class Pmd:

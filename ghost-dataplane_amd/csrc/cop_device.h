@@ -180,7 +180,8 @@ __device__ __forceinline__ uint32_t ivt_search(const uint32_t *S, uint32_t m, ui
 constexpr int LB_GROUPS = 4;
 constexpr uint32_t LB_GAVE_UP = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_t stride, uint32_t j, uint32_t agg,
-                                              uint32_t epoch, uint32_t *err, int lane, const uint32_t *exitw = nullptr)
+                                              uint32_t epoch, uint32_t *err, int lane, const uint32_t *exitw = nullptr,
+                                              uint32_t spin_log2 = 22)
 {
     const unsigned long long ep = (unsigned long long)epoch << 32;
     if (j == 0) {
@@ -224,7 +225,7 @@ __device__ __forceinline__ uint32_t look_back(unsigned long long *chain, uint32_
         if (done) break;
         qhi -= consumed;
         if (consumed == 0) {
-            if (++spins > (1u << 22)) {       // bounded: never hang the GPU
+            if (++spins > (1u << spin_log2)) {   // bounded: never hang the GPU
                 if (lane == 0) *err = 1u;
                 if (exitw) return LB_GAVE_UP; // poll mode: publish nothing, count nothing
                 break;
@@ -853,6 +854,7 @@ struct LookCtx {
     uint32_t epoch;
     uint32_t *err;
     const uint32_t *exitw = nullptr;   // poll-mode kernel: its exit word (look_back)
+    uint32_t spin_log2 = 22;           // look_back's spin bound (tests shorten it)
 };
 
 // LDS scratch of one compaction: per-(step, wave) counts and the prefix of
@@ -958,7 +960,7 @@ __device__ __forceinline__ bool compact_tile(const LookCtx &lk, const Opt &o, co
         if (wave == 0) {
             // dbg bit 32 (timing-only ablation): no look-back wait, wrong offsets
             const uint32_t excl =
-                (o.dbg & 32u) ? j * 1024u : look_back(lk.look + lb_off, 1u, j, agg, lk.epoch, lk.err, lane, lk.exitw);
+                (o.dbg & 32u) ? j * 1024u : look_back(lk.look + lb_off, 1u, j, agg, lk.epoch, lk.err, lane, lk.exitw, lk.spin_log2);
             if (lane == 0) {
                 *s.pref = excl;
                 if (B.fwd_count && j == B.ntiles - 1 && excl != LB_GAVE_UP) st_u32<WT>(excl + agg, B.fwd_count);
@@ -995,7 +997,8 @@ __device__ __forceinline__ bool compact_tile(const LookCtx &lk, const Opt &o, co
         uint32_t agg;
         const uint32_t ex = wave_excl_scan(lane < NQ ? s.dq[q * NQ + lane] : 0u, NQ, lane, &agg);
         if (lane < NQ) s.dq[q * NQ + lane] = ex;
-        const uint32_t excl = look_back(lk.look + (size_t)lb_off * K + q, K, j, agg, lk.epoch, lk.err, lane, lk.exitw);
+        const uint32_t excl = look_back(lk.look + (size_t)lb_off * K + q, K, j, agg, lk.epoch, lk.err, lane, lk.exitw,
+                                         lk.spin_log2);
         if (lane == 0) {
             s.dpref[q] = excl;
             if (B.fwd_count && j == B.ntiles - 1 && excl != LB_GAVE_UP) st_u32<WT>(excl + agg, &B.fwd_count[q]);

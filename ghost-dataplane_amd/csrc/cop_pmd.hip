@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "cop_device.h"
 #include "cop_kernels.h"
 #include "cop_tile.h"
@@ -192,15 +194,14 @@ __device__ __forceinline__ __attribute__((unused)) CopKBatch pmd_batch(const Cop
     return B;
 }
 
-// experiment builds only: COPK_PMD_PF=1 compiles the next-tile L2 prefetch
-// ($COP_PMD_PREFETCH=1 turns it on; its registers spill in production builds)
-#ifndef COPK_PMD_PF
-#define COPK_PMD_PF 0
-#endif
 // experiment builds only: COPK_PMD_WT=0 stores non-temporally (timing of the
 // write-through cost; results are then not guaranteed visible at completion)
 #ifndef COPK_PMD_WT
 #define COPK_PMD_WT 1
+#endif
+// steps of its next tile a worker loads before counting its tile (carry)
+#ifndef COPK_PMD_CARRY
+#define COPK_PMD_CARRY 1
 #endif
 // Workers per CU (waves per SIMD): 4 for 2048-packet tiles (<= 128 VGPRs),
 // 5 for 1024-packet tiles (<= 96), 6 for 256-packet tiles (<= 80; the SGPR
@@ -252,126 +253,167 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
     const uint32_t G = (P.n_work - r + R - 1) / R;
     const CopKRing &rg = P.rings[r];
     const uint32_t rs0 = r * n_slots;   // ring r's first (slot-count, completion, n) word
-    // tile (b, j, slot) of T = seq0r[r]*tpb + wr, advanced by G per step
-    unsigned long long b = P.seq0r[r] + wr / tpb;
-    uint32_t j = wr % tpb;
-    uint32_t slot = (uint32_t)(b % n_slots);
-    const uint32_t qb = G / tpb, rb = G % tpb;
-    unsigned long long posted = 0;
-    const bool leader = wr % P.relay_stride == 0;
-    unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
-    for (;;) {
-        if (stamp && tid == 0) st_stamp(&stamp[0], __builtin_amdgcn_s_memrealtime());   // diagnostic: tile start
-        if (b >= posted) {
-            // wait for batch b to be posted (one lane polls the relay)
-            if (tid == 0) {
-                const unsigned long long hp = wait_posted(P, r, wr, b, leader);
-                s_door[0] = (uint32_t)hp;
-                s_door[1] = (uint32_t)(hp >> 32);
-                s_door[2] = hp == 0 ? 1u : 0u;
-            }
-            lds_barrier();
-            posted = ((unsigned long long)s_door[1] << 32) | s_door[0];
-            const uint32_t leave = s_door[2];
-            lds_barrier();   // s_door is rewritten only after every wave has read it
-            if (leave) break;
-        }
-        if (stamp && tid == 0) {
-            st_stamp(&stamp[1], __builtin_amdgcn_s_memrealtime());   // batch b posted (as seen here)
-            st_stamp(&stamp[4], b);
-        }
-        // the batch's packets: fixed (the ring's n), or the host's count for
-        // the slot (written before the doorbell that posted the batch)
-        uint32_t n = rg.n;
-        if (P.h_n) {
-            if (tid == 0)
-                s_door[3] = __hip_atomic_load(&P.h_n[rs0 + slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            lds_barrier();
-            n = min(s_door[3], rg.n);
-            lds_barrier();
-        }
-        const uint32_t ntiles = (n + TILE - 1) / TILE;
-        // The lane's index is made opaque each iteration, so the per-lane
-        // values the tile derives from it (load geometry, LDS addresses) are
-        // recomputed in the tile rather than hoisted out of the loop and held
-        // live across it: loop-invariant code motion cost the persistent
-        // kernel ~50 VGPRs over the one-shot kernel's tile.
-        int tid_i = tid;
-        asm volatile("" : "+v"(tid_i));
-        const int lane_i = tid_i & 63;
-        const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
-        const uint32_t look_off = (rs0 + slot) * tpb;
-        const CopKBatch B = pmd_batch(p, rg, slot, n, ntiles);
-        bool ok = true;
-        if (j < ntiles) {   // (a tile past a short batch's packets has nothing to do)
-            if (EXT && p.hit_region) {
-                // binned rule hits: the tile's bucket counts start at zero (the
-                // last tile's sort is done with them: the barrier below ordered it)
-                for (uint32_t i = (uint32_t)tid_i; i < p.hit_nb; i += BLOCK) lds[p.lds_hit_off + i] = 0u;
-                lds_barrier();
-            }
-            // tile_steps stores records from lane pairs only (p.rec_paired: every
-            // slot's records 16-byte aligned); other record forms take tile_body
-            if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && p.rec_paired && P.stepwise) {
-                // experiment ($COP_PMD_PREFETCH): once this tile's loads are
-                // out, one plain load per lane of each 128-byte line of the
-                // first two steps of this worker's next tile, if posted, so
-                // its headers sit in L2 when its own loads go out. The value
-                // is consumed after the tile (its wait joins the drain).
-                uint32_t pfv = 0;
-                auto pf = [&] {
-                    if (!COPK_PMD_PF || !P.prefetch) return;
-                    uint32_t j2 = j + rb;
-                    unsigned long long b2 = b + qb;
-                    if (j2 >= tpb) {
-                        j2 -= tpb;
-                        b2++;
-                    }
-                    if (b2 >= posted || P.h_n) return;
-                    uint32_t s2 = slot + (uint32_t)((b2 - b) % n_slots);
-                    if (s2 >= n_slots) s2 -= n_slots;
-                    const uint8_t *pk2 = rg.pkts + (size_t)s2 * rg.pkts_slot_bytes + rg.data_off;
-                    const uint32_t pkt = min(j2 * TILE + (uint32_t)tid_i * 2u, rg.n - 1u);
-                    pfv = *(const uint32_t *)(pk2 + (size_t)pkt * rg.stride);
-                };
-                tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, B, j, tid_i, lane_i, wave_i, pf);
-                if (COPK_PMD_PF) asm volatile("" ::"v"(pfv));
-            } else
-                ok = tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
-                    p, o, lc, B, look_off, j, LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0]}, tid_i,
-                    lane_i, wave_i, false, (size_t)(rs0 + slot) * tpb + j);
-        }
-        // completion: every wave's stores (write-through) and counter adds
-        // have landed, then one lane counts the tile for its slot; the slot's
-        // last tile writes the batch's sequence + 1 to host memory. (One
-        // host-memory word per tile instead was measured: the host saw a
-        // 20-batch post complete ~20 us after its last tile, 1280 PCIe writes
-        // against 20; profiles/r03/first/probe_seg.log.)
-        if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();
-        // (a tile whose look-back gave up, ok false, is not counted: its
-        // batch never completes and the host sees the abort)
-        if (tid == 0 && ok) {
-            const unsigned long long old = atomicAdd(&P.slot_tiles[(size_t)(rs0 + slot) * P.slot_stride], 1ull);
-            if ((old + 1) % tpb == 0)
-                __hip_atomic_store(&P.h_done[rs0 + slot], b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // The serving loop, in two forms (the choice is loop-invariant): tiles
+    // step by step (tile_steps: segmented lists, records from lane pairs, no
+    // optional feature), or tile_body. The step-by-step form carries a
+    // worker's next tile across its completion (below).
+    auto serve = [&](auto steps_c) {
+        constexpr bool STEPS = decltype(steps_c)::value;
+        constexpr int WIN = COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT;
+        constexpr int CARRY = COPK_PMD_CARRY < WIN ? COPK_PMD_CARRY : WIN;
+        // tile (b, j, slot) of T = seq0r[r]*tpb + wr, advanced by G per step
+        unsigned long long b = P.seq0r[r] + wr / tpb;
+        uint32_t j = wr % tpb;
+        uint32_t slot = (uint32_t)(b % n_slots);
+        const uint32_t qb = G / tpb, rb = G % tpb;
+        unsigned long long posted = 0;
+        const bool leader = wr % P.relay_stride == 0;
+        unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
+        // the tile's completion, by one lane once every wave's stores
+        // (write-through) and counter adds have landed: count it for its
+        // slot; the slot's last tile writes the batch's sequence + 1 to host
+        // memory. (One host-memory word per tile instead was measured: the
+        // host saw a 20-batch post complete ~20 us after its last tile, 1280
+        // PCIe writes against 20; profiles/r03/first/probe_seg.log.)
+        auto count_tile = [&](uint32_t sl, unsigned long long bb) {
+            const unsigned long long old = atomicAdd(&P.slot_tiles[(size_t)(rs0 + sl) * P.slot_stride], 1ull);
+            const bool last_tile = (old + 1) % tpb == 0;
+            if (last_tile) __hip_atomic_store(&P.h_done[rs0 + sl], bb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (stamp) {
                 st_stamp(&stamp[3], __builtin_amdgcn_s_memrealtime());   // stores drained, tile counted
-                st_stamp(&stamp[5], (old + 1) % tpb == 0 ? 1ull : 0ull);
+                st_stamp(&stamp[5], last_tile ? 1ull : 0ull);
             }
+        };
+        // T += G
+        auto advance = [&] {
+            j += rb;
+            uint32_t db = qb;
+            if (j >= tpb) {
+                j -= tpb;
+                db++;
+            }
+            b += db;
+            slot += db % n_slots;
+            if (slot >= n_slots) slot -= n_slots;
+        };
+        for (;;) {
+            if (stamp && tid == 0) st_stamp(&stamp[0], __builtin_amdgcn_s_memrealtime());   // diagnostic: tile start
+            if (b >= posted) {
+                // wait for batch b to be posted (one lane polls the relay)
+                if (tid == 0) {
+                    const unsigned long long hp = wait_posted(P, r, wr, b, leader);
+                    s_door[0] = (uint32_t)hp;
+                    s_door[1] = (uint32_t)(hp >> 32);
+                    s_door[2] = hp == 0 ? 1u : 0u;
+                }
+                lds_barrier();
+                posted = ((unsigned long long)s_door[1] << 32) | s_door[0];
+                const uint32_t leave = s_door[2];
+                lds_barrier();   // s_door is rewritten only after every wave has read it
+                if (leave) break;
+            }
+            if (stamp && tid == 0) {
+                st_stamp(&stamp[1], __builtin_amdgcn_s_memrealtime());   // batch b posted (as seen here)
+                st_stamp(&stamp[4], b);
+            }
+            // the batch's packets: fixed (the ring's n), or the host's count for
+            // the slot (written before the doorbell that posted the batch)
+            uint32_t n = rg.n;
+            if (P.h_n) {
+                if (tid == 0)
+                    s_door[3] = __hip_atomic_load(&P.h_n[rs0 + slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                lds_barrier();
+                n = min(s_door[3], rg.n);
+                lds_barrier();
+            }
+            const uint32_t ntiles = (n + TILE - 1) / TILE;
+            // Rings in host memory: the host rewrote the slot since this CU
+            // (or its XCD's L2) may last have read it, and a persistent
+            // kernel gets no dispatch-time cache invalidation, so each tile
+            // acquires at system scope before its loads (the doorbell read
+            // that made the batch visible came first).
+            if (P.sys_acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            // The lane's index is made opaque each iteration, so the per-lane
+            // values the tile derives from it (load geometry, LDS addresses) are
+            // recomputed in the tile rather than hoisted out of the loop and held
+            // live across it: loop-invariant code motion cost the persistent
+            // kernel ~50 VGPRs over the one-shot kernel's tile.
+            int tid_i = tid;
+            asm volatile("" : "+v"(tid_i));
+            const int lane_i = tid_i & 63;
+            const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
+            bool ok = true;
+            if constexpr (STEPS) {
+                if (j < ntiles) {   // (a tile past a short batch's packets has nothing to do)
+                    // Carry ($COP_PMD_CARRY, on by default): while the next
+                    // tile is already posted (a full batch: fixed n), its first
+                    // CARRY steps' loads go out as soon as this tile is done,
+                    // into registers this tile no longer needs, and this tile
+                    // is counted inside the next one once every wave has that
+                    // tile's first step (vmcnt counts in issue order, so this
+                    // tile's stores and counter adds have landed by then): the
+                    // worker's loads stay in flight across its drain and the
+                    // count's round trip. The inner loop starts only here, so
+                    // the carried registers are live across nothing else.
+                    u32x4 v[WIN][3];
+                    CopKBatch B = pmd_batch(p, rg, slot, n, ntiles);
+                    steps_load<PPT, 0, WIN>(B, j, lane_i, wave_i, v);
+                    bool carried = false;
+                    uint32_t cslot = 0;
+                    unsigned long long cb = 0;
+                    for (;;) {
+                        // (opaque again: the lane's values are not hoisted out of this loop)
+                        int tid_c = tid;
+                        asm volatile("" : "+v"(tid_c));
+                        const int lane_c = tid_c & 63;
+                        const int wave_c = __builtin_amdgcn_readfirstlane(tid_c >> 6);
+                        tile_steps_v<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, B, j, tid_c, lane_c, wave_c, v, [&] {
+                            if (carried && tid == 0) count_tile(cslot, cb);
+                        });
+                        if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // body done
+                        cslot = slot;
+                        cb = b;
+                        advance();
+                        carried = P.carry && !P.h_n && !P.sys_acquire && b < posted;
+                        if (!carried) break;
+                        B = pmd_batch(p, rg, slot, rg.n, tpb);
+                        steps_load<PPT, 0, CARRY>(B, j, lane_c, wave_c, v);
+                        steps_load<PPT, CARRY, WIN>(B, j, lane_c, wave_c, v);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    lds_barrier();
+                    if (tid == 0) count_tile(cslot, cb);
+                    continue;
+                }
+            } else {
+                if (P.test_skip && r == 0 && b == 0 && j + 1 == P.test_skip) {
+                    ok = false;   // tests: this tile never runs nor publishes (its successors give up)
+                } else if (j < ntiles) {
+                    if (EXT && p.hit_region) {
+                        // binned rule hits: the tile's bucket counts start at zero (the
+                        // last tile's sort is done with them: the barrier below ordered it)
+                        for (uint32_t i = (uint32_t)tid_i; i < p.hit_nb; i += BLOCK) lds[p.lds_hit_off + i] = 0u;
+                        lds_barrier();
+                    }
+                    ok = tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
+                        p, o, lc, pmd_batch(p, rg, slot, n, ntiles), (rs0 + slot) * tpb, j,
+                        LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0], P.test_skip ? 14u : 22u}, tid_i, lane_i, wave_i, false,
+                        (size_t)(rs0 + slot) * tpb + j);
+                }
+            }
+            if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done
+            // completion (a tile whose look-back gave up, ok false, is not
+            // counted: its batch never completes and the host sees the abort)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_barrier();
+            if (tid == 0 && ok) count_tile(slot, b);
+            advance();
         }
-        // next tile: T += G
-        j += rb;
-        uint32_t db = qb;
-        if (j >= tpb) {
-            j -= tpb;
-            db++;
-        }
-        b += db;
-        slot += db % n_slots;
-        if (slot >= n_slots) slot -= n_slots;
-    }
+    };
+    if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && p.rec_paired && P.stepwise)
+        serve(std::integral_constant<bool, steps_ok<FW, LPM, LAY, EXT>()>{});
+    else
+        serve(std::integral_constant<bool, false>{});
 }
 
 template <int FW, int LPM, int LAY, int PPT>

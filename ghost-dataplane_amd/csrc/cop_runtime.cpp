@@ -1992,6 +1992,7 @@ struct cop_pmd {
     uint8_t *dev = nullptr;                 // device words: ctl, gates, relays, slot tile counts, look-back
     size_t dev_bytes = 0;
     uint32_t n_rings = 1, n_slots = 0, tpb = 0, per_cu = 0, ring_n = 0;
+    bool sys_acquire = false;   // COP_PMD_SYS_ACQUIRE (host-memory rings get it regardless)
     std::atomic<uint32_t> launches{0};
     uint32_t pauses = 0;                    // pmd_pause calls that stopped a running kernel
     bool was_live = false;                  // pmd_pause found it running (pmd_resume relaunches)
@@ -2148,7 +2149,21 @@ static void pmd_size(cop_pmd *m)
     m->P.poll_backoff = 3;
     m->P.stepwise = getenv("COP_PMD_STEPWISE") && !atoi(getenv("COP_PMD_STEPWISE")) ? 0u : 1u;
     if (const char *e = getenv("COP_PMD_BACKOFF")) m->P.poll_backoff = std::min(64u, (uint32_t)atoi(e));
-    m->P.prefetch = getenv("COP_PMD_PREFETCH") && atoi(getenv("COP_PMD_PREFETCH")) ? 1u : 0u;
+    m->P.carry = getenv("COP_PMD_CARRY") && !atoi(getenv("COP_PMD_CARRY")) ? 0u : 1u;
+    // rings whose packets live in host memory (mapped pinned: the drop-in's
+    // header records) are rewritten by the host between batches: a system-
+    // scope acquire before each tile's loads keeps the CU and L2 caches from
+    // serving a slot's previous batch
+    m->P.sys_acquire = m->sys_acquire ? 1u : 0u;
+    for (uint32_t q = 0; q < m->n_rings; q++) {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, m->P.rings[q].pkts) == hipSuccess && at.type == hipMemoryTypeHost)
+            m->P.sys_acquire = 1;
+    }
+    (void)hipGetLastError();   // (an unregistered pointer leaves an error behind)
+    if (const char *e = getenv("COP_PMD_ACQUIRE")) m->P.sys_acquire = atoi(e) != 0;   // A/B runs
+    // tests: a tile that never runs, so its successors' look-back gives up
+    m->P.test_skip = getenv("COP_PMD_TEST_SKIP_TILE") ? (uint32_t)atoi(getenv("COP_PMD_TEST_SKIP_TILE")) + 1u : 0u;
 }
 
 // wait for the launch's census: 0 = every worker resident, 1 = aborted
@@ -2290,7 +2305,7 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
     if (!c || !rings || !out || n_rings < 1) return -EINVAL;
     *out = nullptr;
     if (n_rings > COPK_PMD_MAX_RINGS) return set_err(c, -EINVAL, "pmd: %u rings > %d", n_rings, COPK_PMD_MAX_RINGS);
-    if (flags & ~COP_PMD_VARIABLE_N) return set_err(c, -EINVAL, "pmd: unknown flags %#x", flags);
+    if (flags & ~(COP_PMD_VARIABLE_N | COP_PMD_SYS_ACQUIRE)) return set_err(c, -EINVAL, "pmd: unknown flags %#x", flags);
     if (c->pmd) return set_err(c, -EBUSY, "this context already has a poll-mode kernel");
     const cop_batch_ring *r = &rings[0];
     for (uint32_t q = 0; q < n_rings; q++) {
@@ -2322,6 +2337,7 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
     m->c = c;
     m->n_rings = n_rings;
     m->ring_n = r->n;
+    m->sys_acquire = (flags & COP_PMD_SYS_ACQUIRE) != 0;
     Plan pl = plan_launch(c, (uint64_t)r->n * r->n_slots, imix, r->stride);
     // tile size: 1024-packet tiles (five workers per CU, so a 20-batch burst
     // of 64k packets is one tile per worker), 256-packet tiles for small

@@ -209,11 +209,29 @@ constexpr bool steps_ok()
 #ifndef COPK_PMD_WIN
 #define COPK_PMD_WIN 4
 #endif
-// pf: called once the tile's first loads are issued (the poll-mode kernel's
-// L2 prefetch of its next tile, which then queues behind this tile's loads)
-template <int FW, int LPM, int PPT, bool WT, typename Pf>
-__device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
-                                           int tid, int lane, int wave, Pf pf)
+// The header loads of steps K0 .. K1 - 1 of a tile (of tile_steps_v's
+// window: K1 <= W, all PPT steps when W == PPT): issued, not waited for.
+template <int PPT, int K0, int K1>
+__device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int lane, int wave,
+                                           u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3])
+{
+    static_assert(K1 <= (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT), "steps beyond the window");
+    const StepGeom sg = step_geom(lane);
+    const uint32_t base = j * (BLOCK * PPT);
+    const uint32_t last = B.n ? B.n - 1 : 0u;
+#pragma unroll
+    for (int k = K0; k < K1; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
+}
+
+// v: the tile's first W steps as steps_load issued them. first_step: called
+// by every thread after step 0's barrier — every wave has then waited for
+// its step-0 loads, so (vmcnt counts in issue order) for every memory
+// operation it issued before them: the poll-mode kernel counts its previous
+// tile there, whose stores went out before this tile's loads.
+template <int FW, int LPM, int PPT, bool WT, typename First>
+__device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
+                                             int tid, int lane, int wave,
+                                             u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], First first_step)
 {
     static_assert(COPK_SEG == BLOCK, "one segment per tile step");
     const Tables &tb = lc.tb;
@@ -225,10 +243,6 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
     // gathered, so the CU's queue holds every worker's early steps before
     // any worker's late ones and the workers' last steps land together
     constexpr int W = COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT;
-    u32x4 v[W][3];
-#pragma unroll
-    for (int k = 0; k < W; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
-    pf();
     Counts tot;
     uint32_t *r = (uint32_t *)B.results;
     const int i2 = lane & 31;
@@ -279,6 +293,10 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
             else if (idx < B.n) st_u32x2<WT>(u32x2{a0, a1}, (u32x2 *)&r[2 * (size_t)idx]);
         }
         if (COPK_XP & 4) {
+            if (k == 0) {
+                lds_barrier();
+                first_step();
+            }
             if (k == PPT - 1) {
                 lds_barrier();
                 counters_add(p, lc.s_red, tid);
@@ -286,6 +304,7 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
             continue;
         }
         lds_barrier();
+        if (k == 0) first_step();
         // the step's segment: this wave's forwarded packets after the lower
         // waves' ones, in lane order
         uint32_t off = 0, all = 0;
@@ -302,6 +321,16 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
         if (B.fwd_count && tid == 0 && pk0 < B.n) st_u32<WT>(all, B.fwd_count + pk0 / COPK_SEG);
         if (k == PPT - 1) counters_add(p, lc.s_red, tid);
     }
+}
+
+// One tile of the poll-mode kernel, step by step: loads, then tile_steps_v.
+template <int FW, int LPM, int PPT, bool WT>
+__device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
+                                           int tid, int lane, int wave)
+{
+    u32x4 v[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3];
+    steps_load<PPT, 0, (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT)>(B, j, lane, wave, v);
+    tile_steps_v<FW, LPM, PPT, WT>(p, lc, B, j, tid, lane, wave, v, [] {});
 }
 
 // One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,

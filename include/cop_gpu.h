@@ -442,6 +442,12 @@ int cop_pmd_stop(cop_pmd *pmd);
  * COP_PMD_MAX_RINGS. The single-ring calls above act on ring 0. */
 #define COP_PMD_MAX_RINGS 8
 #define COP_PMD_VARIABLE_N 1u   /* batches carry their own packet count (cop_pmd_post_batch) */
+/* Each tile acquires at system scope before it loads its packets: for rings
+ * whose slots another agent (the host, a NIC, another GPU) rewrites between
+ * batches. A persistent kernel gets no dispatch-time cache invalidation, so
+ * without it a CU or L2 may serve a slot's previous contents. Rings in host
+ * memory get it without the flag. */
+#define COP_PMD_SYS_ACQUIRE 2u
 int cop_pmd_start_rings(cop_ctx *ctx, const cop_batch_ring *rings, uint32_t n_rings, uint32_t flags,
                         cop_pmd **out);
 /* Post the next `count` full batches (n packets each) of one ring. */

@@ -325,3 +325,39 @@ def test_pmd_counter_reduce_while_serving(gpu_ctx_factory, monkeypatch):
         assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
         assert m.info()["launches"] >= 1
     assert all(a < 50 and b < 50 for a, b in times), times
+
+
+def test_pmd_look_back_give_up_completes_nothing(gpu_ctx_factory, monkeypatch):
+    """a dense-list tile whose look-back gives up must not
+    write its list or count, nor be counted for its slot. Tile 1 of batch 0
+    never runs ($COP_PMD_TEST_SKIP_TILE, tests only), so tiles 2.. of that
+    batch wait on a predecessor that never publishes: they time out, give up
+    and the kernel aborts. The batch never completes (the wait reports the
+    abort), its forward count is never written, and past tile 0's own
+    entries the list is untouched."""
+    monkeypatch.setenv("COP_PMD_TEST_SKIP_TILE", "1")
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    B, P = 65536, 2
+    pk = cg.gen_trace(0x5EED0B80, B * P, rules)
+    rg = Ring(ctx, pk, B, P)
+    rg.df.fill(0xFF)
+    m = ctx.pmd_start(rg.ring)
+    tpb = m.info()["tiles_per_batch"]
+    try:
+        m.post(1)
+        with pytest.raises(cg.CopError):
+            m.wait()
+        assert m.info()["state"] == 3          # aborted
+    finally:
+        try:
+            m.stop()
+        except cg.CopError:
+            pass
+    _, fwd, cnt = rg.read()
+    assert int(cnt[0]) == 0xFFFFFFFF          # the last tile gave up: no count
+    _, fos = oracle_slots(pk[:B * 64], B, 1, S | F, oracle_tables(rules)[0])
+    c0 = int(np.sum(fos[0] < B // tpb))       # tile 0's forwarded packets
+    assert np.array_equal(fwd[:c0], fos[0][:c0])
+    assert (fwd[c0:B] == 0xFFFFFFFF).all()

@@ -198,3 +198,32 @@ def test_hdr16_rings_variable_n(gpu_ctx_factory, stages):
                 res = bufs[r][1].download(cg.RESULT_DT, B * P)[s_ * B:s_ * B + n]
                 ro, _, _ = orc.process(pks[r][s_ * B * 64:(s_ * B + n) * 64], n, stages=stages, fw=fw)
                 assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"ring {r} batch {i} (n={n})"
+
+
+def test_slots_rewritten_between_batches(gpu_ctx_factory):
+    """A producer that rewrites ring slots between batches (here the host,
+    by copies into HBM; on a real deployment a NIC): with COP_PMD_SYS_ACQUIRE
+    each tile acquires before its loads, so a slot's new packets are read,
+    never the previous batch's that a CU or L2 may still hold. Eight
+    generations through a two-slot ring, records and lists per batch."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    fw, _ = oracle_tables(rules)
+    B, P = 65536, 2
+    gens = [cg.gen_trace(0x5EED7500 + g, B, rules) for g in range(8)]
+    rg = SegRing(ctx, np.concatenate([gens[0], gens[1]]), B, P)
+    with ctx.pmd_start(rg.ring, cg.PMD_SYS_ACQUIRE) as m:
+        for g in range(8):
+            s_ = g % P
+            if g >= P:
+                rg.dp.upload(gens[g], s_ * B * 64)
+            m.post(1)
+            m.wait()
+            res = rg.dr.download(cg.RESULT_DT, B * P)[s_ * B:(s_ + 1) * B]
+            fwd = rg.df.download(np.uint32, B * P)[s_ * B:(s_ + 1) * B]
+            cnt = rg.dc.download(np.uint32, P * nseg(B))[s_ * nseg(B):(s_ + 1) * nseg(B)]
+            ro, fo = oracle_batch(gens[g], B, S | F, fw)
+            assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"generation {g}"
+            assert np.array_equal(seg_to_dense(fwd, cnt, B), fo), f"generation {g} list"
+        assert m.info()["launches"] == 1   # served by one launch: no relaunch invalidated the caches
