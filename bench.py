@@ -221,7 +221,7 @@ def table_probes(fw_tab, rt_tab, sample, imix_offsets, route_form):
         if form == "bkt":
             # one 8-byte index load + one 16-byte pair load per reaching
             # packet, plus the wide-bucket rounds (two 16-byte loads each)
-            _, _, info = tab.bkt_probe(key[reach], 0)
+            _, _, info = tab.bkt_probe(key[reach], 0, int(os.environ.get("COP_BKT_XBITS", "1")))
             out[name] = {"form": "bkt (bucketed intervals, L2)", "ib": info["ib"],
                          "l2_loads_per_pkt": round((2 * float(reach.sum()) + 2 * info["rounds"]) / n, 4),
                          "wide_lookups_per_pkt": round(info["lifted"] / n, 4),

@@ -590,56 +590,64 @@ __device__ __forceinline__ void tbl8_step(const uint32_t *tbl8, uint32_t packed,
 
 // The bucketed route form's second round (COPK_TBL_BKT, lpm_bkt.c): for
 // each reached packet with candidates k0..k1 (start k0 <= ip, R(ip) <= k1),
-// one 16-byte load of pairs k0 and k0 + 1 decides when ip is below start
-// k0 + 1 or k1 <= k0 + 1 (all PPT loads issued before any is used). Lanes in
-// a wider bucket then scan on, four pairs (two 16-byte loads) a round, until
-// a start above ip or k1: a wave that holds any such lane pays about one
-// more round, not a binary search's lv dependent loads.
+// one 64-byte read of pairs k0 .. k0 + 7 (four 16-byte loads, all PPT
+// packets' issued before any is used) decides every lookup whose bucket
+// holds at most 7 boundaries; lanes in a wider bucket (rare) scan on, two
+// pairs (one 16-byte load) a round, until a start above ip or k1. So a
+// wave's lookups take two dependent L2 rounds, the index and the pairs,
+// where a search that read one pair per round paid a third and fourth
+// round for the wave's densest bucket.
 // e[k] <- the interval's value (the rte_lpm entry form: bit 24 hit, nh).
 template <int PPT>
 __device__ __forceinline__ void bkt_step(const uint32_t *pairs, const uint32_t (&ip)[PPT], uint32_t (&e)[PPT],
                                          const uint32_t (&k1)[PPT], const bool (&live)[PPT])
 {
-    u32x4a q[PPT];
+    u32x4a q[PPT][4];
 #pragma unroll
     for (int k = 0; k < PPT; k++)
-        if (live[k]) q[k] = *(const u32x4a *)(pairs + 2 * (size_t)e[k]);
+        if (live[k]) {
+            const uint32_t *b = pairs + 2 * (size_t)e[k];
+#pragma unroll
+            for (int h = 0; h < 4; h++) q[k][h] = *(const u32x4a *)(b + 4 * h);
+        }
     bool more[PPT];
+    uint32_t nxt[PPT];
     bool any = false;
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         more[k] = false;
+        nxt[k] = 0;
         if (!live[k]) continue;
-        const uint32_t k0 = e[k];
-        const bool up = ip[k] >= q[k].z;   // start k0 + 1 (a pad of 0xFFFFFFFF past the end)
-        more[k] = up && k1[k] > k0 + 1u;
-        any |= more[k];
-        e[k] = up ? q[k].w : q[k].y;
-        if (more[k]) q[k].x = k0 + 2u;     // the next pair to look at
-    }
-    // the rare wide bucket: pairs j .. j + 3 per round (pads past the end
-    // hold start 0xFFFFFFFF; j <= k1 <= m - 1, so j + 3 < m + 4)
-    while (__ballot(any)) {
-        u32x4a a[PPT], b[PPT];
+        const uint32_t k0 = e[k], w = k1[k] - k0;   // candidates k0 .. k0 + w
+        uint32_t v = q[k][0].y;                      // start k0 <= ip always
 #pragma unroll
-        for (int k = 0; k < PPT; k++) {
-            if (more[k]) {
-                a[k] = *(const u32x4a *)(pairs + 2 * (size_t)q[k].x);
-                b[k] = *(const u32x4a *)(pairs + 2 * (size_t)q[k].x + 4);
-            }
+        for (int t = 1; t < 8; t++) {
+            const u32x4a &c = q[k][t >> 1];
+            const uint32_t st = (t & 1) ? c.z : c.x, va = (t & 1) ? c.w : c.y;
+            if (w >= (uint32_t)t && ip[k] >= st) v = va;
         }
+        e[k] = v;
+        more[k] = w > 7u && ip[k] >= q[k][3].z;      // start k0 + 7 <= ip: the answer lies further on
+        nxt[k] = k0 + 8u;
+        any |= more[k];
+    }
+    // the wide bucket: pairs j, j + 1 per round (pads past the end hold
+    // start 0xFFFFFFFF; j <= k1 <= m - 1, so j + 1 < m + 8)
+    while (__ballot(any)) {
+        u32x4a c[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++)
+            if (more[k]) c[k] = *(const u32x4a *)(pairs + 2 * (size_t)nxt[k]);
         any = false;
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
             if (!more[k]) continue;
-            const uint32_t j = q[k].x, hi = k1[k];
-            if (ip[k] >= a[k].x) e[k] = a[k].y;                       // j <= k1 always
-            if (j + 1u <= hi && ip[k] >= a[k].z) e[k] = a[k].w;
-            if (j + 2u <= hi && ip[k] >= b[k].x) e[k] = b[k].y;
-            if (j + 3u <= hi && ip[k] >= b[k].z) e[k] = b[k].w;
-            more[k] = j + 3u < hi && ip[k] >= b[k].z;
+            const uint32_t j = nxt[k], hi = k1[k];
+            if (ip[k] >= c[k].x) e[k] = c[k].y;        // j <= k1 always
+            if (j + 1u <= hi && ip[k] >= c[k].z) e[k] = c[k].w;
+            more[k] = j + 1u < hi && ip[k] >= c[k].z;
             any |= more[k];
-            q[k].x = j + 4u;
+            nxt[k] = j + 2u;
         }
     }
 }

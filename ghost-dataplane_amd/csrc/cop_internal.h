@@ -91,7 +91,7 @@ int cop_lpm_trie_probe(const cop_lpm_table *tab, int form, const uint32_t *ips, 
  * first-candidate positions, pairs = (start, value) x (m + COP_BKT_PADS) */
 #define COP_BKT_MIN_BITS 12u
 #define COP_BKT_MAX_BITS 22u
-#define COP_BKT_PADS 4u
+#define COP_BKT_PADS 8u
 #define COP_BKT_XBITS 1u   /* default: 2 buckets per interval */
 typedef struct {
     uint32_t m, ib, lv, widest;

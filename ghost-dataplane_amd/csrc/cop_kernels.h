@@ -190,7 +190,6 @@ struct CopKPmd {
     uint32_t n_work;                     // worker workgroups
     uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
     uint32_t stepwise;                   // tiles step by step where tile_steps applies ($COP_PMD_STEPWISE=0: off)
-    uint32_t carry;                      // a worker issues its next posted tile's loads before counting this one ($COP_PMD_CARRY)
     uint32_t sys_acquire;                // rings in host memory: a system-scope acquire before each tile's loads
     uint32_t test_skip;                  // tests: tile test_skip - 1 of ring 0's batch 0 never runs ($COP_PMD_TEST_SKIP_TILE)
     uint32_t poll_backoff;               // waiting workers' s_sleep(4) rounds between relay polls once idle

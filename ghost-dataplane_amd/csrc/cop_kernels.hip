@@ -64,8 +64,11 @@ __device__ __forceinline__ __attribute__((unused)) unsigned long long ticket_tak
     return old;
 }
 
+// the bucketed route form at 4 packets per lane sits just above 96 VGPRs:
+// held to 96, it runs 5 waves per SIMD instead of 4
 template <int FW, int LPM, int LAY, int PPT, bool EXT>
-__global__ __launch_bounds__(BLOCK, EXT ? 4 : COPK_WAVES_PER_EU) void cop_pipeline(const CopKParams p)
+__global__ __launch_bounds__(BLOCK, EXT ? 4 : (LPM == COPK_TBL_BKT && PPT == 4) ? 5 : COPK_WAVES_PER_EU) void
+cop_pipeline(const CopKParams p)
 {
     const Opt o = EXT ? opt_all(p) : Opt{0u, 0u, 0u, nullptr};
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];

@@ -199,10 +199,6 @@ __device__ __forceinline__ __attribute__((unused)) CopKBatch pmd_batch(const Cop
 #ifndef COPK_PMD_WT
 #define COPK_PMD_WT 1
 #endif
-// steps of its next tile a worker loads before counting its tile (carry)
-#ifndef COPK_PMD_CARRY
-#define COPK_PMD_CARRY 1
-#endif
 // Workers per CU (waves per SIMD): 4 for 2048-packet tiles (<= 128 VGPRs),
 // 5 for 1024-packet tiles (<= 96), 6 for 256-packet tiles (<= 80; the SGPR
 // limit admits no more, MI355X_MICROARCH.md Residency)
@@ -255,12 +251,10 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
     const uint32_t rs0 = r * n_slots;   // ring r's first (slot-count, completion, n) word
     // The serving loop, in two forms (the choice is loop-invariant): tiles
     // step by step (tile_steps: segmented lists, records from lane pairs, no
-    // optional feature), or tile_body. The step-by-step form carries a
-    // worker's next tile across its completion (below).
+    // optional feature), or tile_body. Two loops, so neither form's
+    // registers are live through the other.
     auto serve = [&](auto steps_c) {
         constexpr bool STEPS = decltype(steps_c)::value;
-        constexpr int WIN = COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT;
-        constexpr int CARRY = COPK_PMD_CARRY < WIN ? COPK_PMD_CARRY : WIN;
         // tile (b, j, slot) of T = seq0r[r]*tpb + wr, advanced by G per step
         unsigned long long b = P.seq0r[r] + wr / tpb;
         uint32_t j = wr % tpb;
@@ -344,47 +338,9 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
             bool ok = true;
             if constexpr (STEPS) {
-                if (j < ntiles) {   // (a tile past a short batch's packets has nothing to do)
-                    // Carry ($COP_PMD_CARRY, on by default): while the next
-                    // tile is already posted (a full batch: fixed n), its first
-                    // CARRY steps' loads go out as soon as this tile is done,
-                    // into registers this tile no longer needs, and this tile
-                    // is counted inside the next one once every wave has that
-                    // tile's first step (vmcnt counts in issue order, so this
-                    // tile's stores and counter adds have landed by then): the
-                    // worker's loads stay in flight across its drain and the
-                    // count's round trip. The inner loop starts only here, so
-                    // the carried registers are live across nothing else.
-                    u32x4 v[WIN][3];
-                    CopKBatch B = pmd_batch(p, rg, slot, n, ntiles);
-                    steps_load<PPT, 0, WIN>(B, j, lane_i, wave_i, v);
-                    bool carried = false;
-                    uint32_t cslot = 0;
-                    unsigned long long cb = 0;
-                    for (;;) {
-                        // (opaque again: the lane's values are not hoisted out of this loop)
-                        int tid_c = tid;
-                        asm volatile("" : "+v"(tid_c));
-                        const int lane_c = tid_c & 63;
-                        const int wave_c = __builtin_amdgcn_readfirstlane(tid_c >> 6);
-                        tile_steps_v<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, B, j, tid_c, lane_c, wave_c, v, [&] {
-                            if (carried && tid == 0) count_tile(cslot, cb);
-                        });
-                        if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // body done
-                        cslot = slot;
-                        cb = b;
-                        advance();
-                        carried = P.carry && !P.h_n && !P.sys_acquire && b < posted;
-                        if (!carried) break;
-                        B = pmd_batch(p, rg, slot, rg.n, tpb);
-                        steps_load<PPT, 0, CARRY>(B, j, lane_c, wave_c, v);
-                        steps_load<PPT, CARRY, WIN>(B, j, lane_c, wave_c, v);
-                    }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    lds_barrier();
-                    if (tid == 0) count_tile(cslot, cb);
-                    continue;
-                }
+                if (j < ntiles)   // (a tile past a short batch's packets has nothing to do)
+                    tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, pmd_batch(p, rg, slot, n, ntiles), j, tid_i,
+                                                                lane_i, wave_i);
             } else {
                 if (P.test_skip && r == 0 && b == 0 && j + 1 == P.test_skip) {
                     ok = false;   // tests: this tile never runs nor publishes (its successors give up)
@@ -395,10 +351,12 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                         for (uint32_t i = (uint32_t)tid_i; i < p.hit_nb; i += BLOCK) lds[p.lds_hit_off + i] = 0u;
                         lds_barrier();
                     }
+                    // (tests shorten the look-back's spin bound: the skipped
+                    // tile's successors give up in well under a second)
+                    const LookCtx lk{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0], P.test_skip ? 14u : 22u};
                     ok = tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
-                        p, o, lc, pmd_batch(p, rg, slot, n, ntiles), (rs0 + slot) * tpb, j,
-                        LookCtx{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0], P.test_skip ? 14u : 22u}, tid_i, lane_i, wave_i, false,
-                        (size_t)(rs0 + slot) * tpb + j);
+                        p, o, lc, pmd_batch(p, rg, slot, n, ntiles), (rs0 + slot) * tpb, j, lk, tid_i, lane_i, wave_i,
+                        false, (size_t)(rs0 + slot) * tpb + j);
                 }
             }
             if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done

@@ -680,11 +680,11 @@ static int upload_bkt(cop_ctx *c, DevLpm &t, const uint32_t *s, const uint32_t *
     cop_lpm_bkt bk;
     int rc = cop_lpm_bkt_build(s, v, m, c->bkt_xbits, &bk);
     if (rc) return set_err(c, rc, "bucketed route form build failed: %d", rc);
-    const size_t ib = ((size_t)(1u << bk.ib) + 1) * 4, pb = 2 * ((size_t)m + COP_BKT_PADS) * 4;
-    hipError_t e = hipMalloc(&t.bidx, ib);
-    if (e == hipSuccess) e = hipMalloc(&t.bpairs, pb);
-    if (e == hipSuccess) e = hipMemcpy(t.bidx, bk.idx, ib, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(t.bpairs, bk.pairs, pb, hipMemcpyHostToDevice);
+    const size_t idx_bytes = ((size_t)(1u << bk.ib) + 1) * 4, pair_bytes = 2 * ((size_t)m + COP_BKT_PADS) * 4;
+    hipError_t e = hipMalloc(&t.bidx, idx_bytes);
+    if (e == hipSuccess) e = hipMalloc(&t.bpairs, pair_bytes);
+    if (e == hipSuccess) e = hipMemcpy(t.bidx, bk.idx, idx_bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(t.bpairs, bk.pairs, pair_bytes, hipMemcpyHostToDevice);
     t.ib = bk.ib;
     t.lv = bk.lv;
     t.b_m = m;
@@ -880,6 +880,10 @@ static int choose_ppt(const cop_ctx *c, uint64_t total, bool imix)
     int ppt = 1;
     if (total >= (uint64_t)COPK_BLOCK * 8 * c->ncu) ppt = imix ? 4 : 8;
     else if (total >= (uint64_t)COPK_BLOCK * 4 * c->ncu) ppt = 4;
+    // the bucketed route form reads 64 bytes of pairs per packet in one
+    // round: at 8 packets per lane that needs 195 VGPRs (2 waves per SIMD),
+    // at 4, 98 (4 waves)
+    if (c->lpm.bidx && ppt > 4) ppt = 4;
     if (c->ppt_override) ppt = c->ppt_override;
     return ppt;
 }
@@ -2149,7 +2153,6 @@ static void pmd_size(cop_pmd *m)
     m->P.poll_backoff = 3;
     m->P.stepwise = getenv("COP_PMD_STEPWISE") && !atoi(getenv("COP_PMD_STEPWISE")) ? 0u : 1u;
     if (const char *e = getenv("COP_PMD_BACKOFF")) m->P.poll_backoff = std::min(64u, (uint32_t)atoi(e));
-    m->P.carry = getenv("COP_PMD_CARRY") && !atoi(getenv("COP_PMD_CARRY")) ? 0u : 1u;
     // rings whose packets live in host memory (mapped pinned: the drop-in's
     // header records) are rewritten by the host between batches: a system-
     // scope acquire before each tile's loads keeps the CU and L2 caches from

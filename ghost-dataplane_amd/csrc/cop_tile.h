@@ -223,15 +223,11 @@ __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int l
     for (int k = K0; k < K1; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
 }
 
-// v: the tile's first W steps as steps_load issued them. first_step: called
-// by every thread after step 0's barrier — every wave has then waited for
-// its step-0 loads, so (vmcnt counts in issue order) for every memory
-// operation it issued before them: the poll-mode kernel counts its previous
-// tile there, whose stores went out before this tile's loads.
-template <int FW, int LPM, int PPT, bool WT, typename First>
+// v: the tile's first W steps as steps_load issued them.
+template <int FW, int LPM, int PPT, bool WT>
 __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
                                              int tid, int lane, int wave,
-                                             u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], First first_step)
+                                             u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3])
 {
     static_assert(COPK_SEG == BLOCK, "one segment per tile step");
     const Tables &tb = lc.tb;
@@ -293,10 +289,6 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
             else if (idx < B.n) st_u32x2<WT>(u32x2{a0, a1}, (u32x2 *)&r[2 * (size_t)idx]);
         }
         if (COPK_XP & 4) {
-            if (k == 0) {
-                lds_barrier();
-                first_step();
-            }
             if (k == PPT - 1) {
                 lds_barrier();
                 counters_add(p, lc.s_red, tid);
@@ -304,7 +296,6 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
             continue;
         }
         lds_barrier();
-        if (k == 0) first_step();
         // the step's segment: this wave's forwarded packets after the lower
         // waves' ones, in lane order
         uint32_t off = 0, all = 0;
@@ -330,7 +321,7 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
 {
     u32x4 v[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3];
     steps_load<PPT, 0, (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT)>(B, j, lane, wave, v);
-    tile_steps_v<FW, LPM, PPT, WT>(p, lc, B, j, tid, lane, wave, v, [] {});
+    tile_steps_v<FW, LPM, PPT, WT>(p, lc, B, j, tid, lane, wave, v);
 }
 
 // One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,

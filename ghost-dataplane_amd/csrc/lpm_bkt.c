@@ -11,9 +11,10 @@
  * 2^ib >= m a bucket holds about one boundary, so the kernel's two rounds
  * (cop_device.h bkt_issue / bkt_step) decide almost every lookup:
  *   1. one 8-byte load {idx[b], idx[b + 1]} = {k0, k1};
- *   2. one 16-byte load of pairs k0 and k0 + 1 = {s0, v0, s1, v1}: the
- *      answer is v0 if ip < s1, v1 if ip >= s1 and k1 <= k0 + 1;
- *   otherwise a scan on over pairs k0 + 2 .. k1, four a round.
+ *   2. one 64-byte read of pairs k0 .. k0 + 7: the answer when the bucket
+ *      holds at most 7 boundaries (k1 <= k0 + 7) or ip lies below start
+ *      k0 + 7;
+ *   otherwise a scan on over pairs k0 + 8 .. k1, two (one 16-byte load) a round.
  * Pairs past the end are pads {0xFFFFFFFF, last value}: only ip 0xFFFFFFFF
  * reaches one, and its answer is the last interval's value. */
 #include <errno.h>
@@ -72,15 +73,16 @@ uint32_t cop_lpm_bkt_lookup(const cop_lpm_bkt *t, uint32_t ip, uint32_t *rounds)
     const uint32_t b = ip >> (32u - t->ib);
     const uint32_t k0 = t->idx[b], k1 = t->idx[b + 1];
     const uint32_t *q = t->pairs + 2 * (size_t)k0;
-    if (ip < q[2]) return q[1];
-    uint32_t e = q[3];
-    if (k1 <= k0 + 1u) return e;
-    for (uint32_t j = k0 + 2u;; j += 4u) {   /* four pairs a round */
+    uint32_t e = q[1];
+    for (uint32_t i = 1; i < 8; i++)   /* pairs k0 .. k0 + 7: one 64-byte read */
+        if (i <= k1 - k0 && ip >= q[2 * i]) e = q[2 * i + 1];
+    if (!(k1 - k0 > 7u && ip >= q[14])) return e;
+    for (uint32_t j = k0 + 8u;; j += 2u) {   /* the wide bucket: two pairs a round */
         const uint32_t *a = t->pairs + 2 * (size_t)j;
         if (rounds) (*rounds)++;
-        for (uint32_t i = 0; i < 4; i++)
+        for (uint32_t i = 0; i < 2; i++)
             if (j + i <= k1 && ip >= a[2 * i]) e = a[2 * i + 1];
-        if (!(j + 3u < k1 && ip >= a[6])) return e;
+        if (!(j + 1u < k1 && ip >= a[2])) return e;
     }
 }
 
