@@ -199,6 +199,9 @@ __device__ __forceinline__ __attribute__((unused)) CopKBatch pmd_batch(const Cop
 #ifndef COPK_PMD_WT
 #define COPK_PMD_WT 1
 #endif
+#ifndef COPK_PMD_RELEASE
+#define COPK_PMD_RELEASE 0
+#endif
 // Workers per CU (waves per SIMD): 4 for 2048-packet tiles (<= 128 VGPRs),
 // 5 for 1024-packet tiles (<= 96), 6 for 256-packet tiles (<= 80; the SGPR
 // limit admits no more, MI355X_MICROARCH.md Residency)
@@ -364,7 +367,16 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             // counted: its batch never completes and the host sees the abort)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             lds_barrier();
-            if (tid == 0 && ok) count_tile(slot, b);
+            if (tid == 0 && ok) {
+                // experiment builds (COPK_PMD_RELEASE with COPK_PMD_WT=0):
+                // plain stores, then one agent-scope release per tile
+                // (the XCD's L2 written back) before the count
+                if (COPK_PMD_RELEASE) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                count_tile(slot, b);
+            }
             advance();
         }
     };

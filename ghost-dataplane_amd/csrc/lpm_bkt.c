@@ -28,7 +28,7 @@ int cop_lpm_bkt_build(const uint32_t *s, const uint32_t *v, uint32_t m, uint32_t
     memset(out, 0, sizeof(*out));
     if (!m || xbits > 8) return -EINVAL;
     uint32_t ib = 0;
-    while ((1u << ib) < m && ib < 32) ib++;
+    while (ib < 31 && (1u << ib) < m) ib++;
     ib += xbits;   /* 2^xbits buckets per interval: fewer wide buckets, a larger index */
     if (ib < COP_BKT_MIN_BITS) ib = COP_BKT_MIN_BITS;
     if (ib > COP_BKT_MAX_BITS) ib = COP_BKT_MAX_BITS;

@@ -16,4 +16,6 @@ for f in dir bkt; do
   step 200 "$out/imix_${f}.log" python3 -u $R/bench.py --workload fw_lpm_imix --steps 1024 --warmup 256 --no-cpu --secondary none --route-form $f
   grep -h '^{"metric"' "$out/imix_${f}.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print("imix", sys.argv[1], d["value"], "frac", r["frac"], "kernel_ms", r["kernel_ms_per_launch"])' "$f"
 done
+cd "$R" && step 500 "$out/ab_wt.log" bash tools/ab_pmd.sh "$out/wt" "wt:" "nowt:COP_LIB=$R/ghost-dataplane_amd/libcopgpu_nowt.so" "wt2:" "nowt2:COP_LIB=$R/ghost-dataplane_amd/libcopgpu_nowt.so"
+tail -4 "$out/ab_wt.log"
 echo done
