@@ -209,6 +209,10 @@ constexpr bool steps_ok()
 #ifndef COPK_PMD_WIN
 #define COPK_PMD_WIN 4
 #endif
+// the step's forward-list segment through LDS and out as 16-byte stores
+#ifndef COPK_PMD_STAGE_LIST
+#define COPK_PMD_STAGE_LIST 1
+#endif
 // The header loads of steps K0 .. K1 - 1 of a tile (of tile_steps_v's
 // window: K1 <= W, all PPT steps when W == PPT): issued, not waited for.
 template <int PPT, int K0, int K1>
@@ -224,7 +228,7 @@ __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int l
 }
 
 // v: the tile's first W steps as steps_load issued them.
-template <int FW, int LPM, int PPT, bool WT>
+template <int FW, int LPM, int PPT, bool WT, bool STAGE_LIST = COPK_PMD_STAGE_LIST>
 __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
                                              int tid, int lane, int wave,
                                              u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3])
@@ -242,6 +246,18 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
     Counts tot;
     uint32_t *r = (uint32_t *)B.results;
     const int i2 = lane & 31;
+    // Staged lists: each step's forward-list segment is written into LDS and
+    // leaves as 16-byte stores (whole chunks, the last clamped to n) once a
+    // later barrier has ordered it. Write-through stores of single words,
+    // one per forwarded lane, cost the poll-mode kernel's steady state 9 %.
+    const bool staged = STAGE_LIST && B.fwd_idx && lc.cl.stage && !(COPK_XP & 4);
+    uint32_t all_prev = 0;
+    auto flush = [&](int k, uint32_t len) {
+        const uint32_t cc = (uint32_t)wave * 16u + (uint32_t)(lane & 15);
+        const uint32_t pk = base + (uint32_t)k * BLOCK;
+        if (lane < 16 && cc * 4u < len)
+            st_list_chunk<WT>(&lc.cl.stage[k * BLOCK + cc * 4u], B.fwd_idx, pk + cc * 4u, B.n);
+    };
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         uint32_t w3[1], w6[1], w7[1], w8[1];
@@ -305,12 +321,23 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
             off += w < wave ? cw : 0u;
             all += cw;
         }
-        if (B.fwd_idx && ((bal >> lane) & 1ull))
-            st_u32<WT>(pk0 + tid, &B.fwd_idx[pk0 + off +
-                                            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))]);
+        const uint32_t rank = off + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (staged) {
+            // the segment's list through LDS; it goes out after the next
+            // step's barrier (the last one's after the loop)
+            if (k > 0) flush(k - 1, all_prev);
+            if ((bal >> lane) & 1ull) lc.cl.stage[k * BLOCK + rank] = pk0 + tid;
+            all_prev = all;
+        } else if (B.fwd_idx && ((bal >> lane) & 1ull)) {
+            st_u32<WT>(pk0 + tid, &B.fwd_idx[pk0 + rank]);
+        }
         if (B.fwd_count && tid == 0 && pk0 < B.n) st_u32<WT>(all, B.fwd_count + pk0 / COPK_SEG);
         if (k == PPT - 1) counters_add(p, lc.s_red, tid);
+    }
+    if (staged) {
+        lds_barrier();
+        flush(PPT - 1, all_prev);
     }
 }
 
