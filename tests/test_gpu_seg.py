@@ -381,3 +381,31 @@ def test_pmd_idle_exit_counts_every_batch_once(gpu_ctx_factory, monkeypatch):
     for b in range(posted):
         want += per_slot[b % P]
     assert np.array_equal(ctx.rule_counters(), want)
+
+
+@pytest.mark.parametrize("fw_dir", [False, True])
+def test_pmd_seg_fw_lpm_dir_probes(gpu_ctx_factory, fw_dir):
+    """The poll-mode kernel with segmented lists and DIR-24-8 stages (they
+    run in tile_body: a step-by-step form with the probes one step ahead
+    was bit-exact but slower): FW + LPM 100k with the
+    route stage in HBM, and with the firewall forced to DIR-24-8 too; a
+    post of every slot, then posts of 1, 5 and 12 batches that wrap the
+    6-slot ring."""
+    rules = fw1k()
+    rts = cg.gen_rules(0x5EED2004, 100000, cg.GEN_ROUTES, 0)
+    ctx = gpu_ctx_factory(stages=S | F | L,
+                          flags=cg.CFG_SEG_LISTS | (cg.CFG_FW_FORCE_DIR24 if fw_dir else 0))
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    ctx.set_route_lpm(cg.LpmTable(rts, 1 << 20, 1 << 16, False))
+    fw, rt = oracle_tables(rules, rts)
+    B, P = 65536, 6
+    pk = cg.gen_trace(0x5EED5E20 + fw_dir, B * P, rules, rts)
+    rg = SegRing(ctx, pk, B, P)
+    with ctx.pmd_start(rg.ring) as m:
+        for k in (P, 1, 5, 12):
+            while k:
+                m.post(min(k, P))
+                k -= min(k, P)
+            m.wait()
+            rg.check(pk, S | F | L, fw, rt)
+        assert m.info()["launches"] == 1
