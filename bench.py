@@ -256,9 +256,11 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def measure(args, name, rank, world, dev, group, primary):
+def measure(args, name, rank, world, dev, group, gate, primary):
     """Time `args.steps` steps of workload `name` (+ its kernel roofline);
-    returns (result dict, context). The caller closes the context."""
+    returns (result dict, context). The caller closes the context. Every
+    timed run opens through the start gate (all ranks' windows at once,
+    CLOCK_MONOTONIC stamps: copdist.StartGate)."""
     W = WORKLOADS[name]
     B = W["batch"]
     Lb = max(1, (args.per_launch if primary else 0) or W["per_launch"])
@@ -292,6 +294,10 @@ def measure(args, name, rank, world, dev, group, primary):
             coll = "ok"
         except Exception as e:  # noqa: BLE001 (reported per rank; the reduce is then skipped)
             coll = f"error: {str(e)[:120]}"
+        # the all-reduce is collective: every rank runs it or none does (a
+        # rank that failed its init would leave the others in RCCL forever)
+        if group.min(1.0 if coll == "ok" else 0.0) < 1.0 and coll == "ok":
+            coll = "skipped: another rank's RCCL init failed"
     rt_tab = None
     if routes is not None:
         rt_tab = cg.LpmTable(routes, max(W["routes"], 1), 1 << 20, False)
@@ -340,10 +346,15 @@ def measure(args, name, rank, world, dev, group, primary):
 
     pmd = None
 
+    # the pool is written once before the kernel starts and never again:
+    # declared (COP_PMD_STATIC_SLOTS), so no tile pays the reuse acquire
+    # (--slots reuse: the default acquire once the ring wraps; always: every tile)
+    pmd_flags = {"static": cg.PMD_STATIC_SLOTS, "reuse": 0, "always": cg.PMD_SYS_ACQUIRE}[args.slots]
+
     def pmd_on():
         nonlocal pmd
         if engine == "pmd" and pmd is None:
-            pmd = ctx.pmd_start(ring)
+            pmd = ctx.pmd_start(ring, pmd_flags)
 
     def pmd_off():
         nonlocal pmd
@@ -374,38 +385,42 @@ def measure(args, name, rank, world, dev, group, primary):
     # the median run (median of 5 runs) ----
     pmd_on()
     run_steps(0, args.warmup)
-    runs, own_runs, reduce_runs, reduce_ms = [], [], [], []
-    red_tot = None
+    runs, own_runs, reduce_runs, reduce_ms, windows = [], [], [], [], []
     for r in range(max(1, args.repeats)):
         pmd_on()
         sync_all()
         group.barrier()
         sync_all()
-        t0 = time.perf_counter()
+        t0 = gate.open()   # every rank's window opens here at once
         run_steps(args.warmup + r * args.steps, args.steps)
+        sync_all()
+        t1 = copdist.monotonic_ns()
         if rc_on and coll == "ok":
-            # one reporting interval: read-and-zero the counters + per-rule
-            # hits and sum them over all GPUs (RCCL beside the running
-            # poll-mode kernel: an atomic exchange, then the all-reduce)
+            # one reporting interval, after the window and timed on its own:
+            # read-and-zero the counters + per-rule hits and sum them over
+            # all GPUs (RCCL; the poll-mode kernel is paused around it). The
+            # reference reads and zeroes its counters every PRINT_DELAY = 2 s
+            # (switch.h:23, switch.c:517-521): far fewer reduces than one per
+            # 20-step window
             r0 = time.perf_counter()
             tot, _ = ctx.coll_reduce_counters(reset=True, with_rules=False)
             reduce_ms.append((time.perf_counter() - r0) * 1e3)
             reduce_runs.append(int(tot["rx"]))
-            if red_tot is None:
-                red_tot = tot   # the first interval also holds the warmup
-        sync_all()
-        t1 = time.perf_counter()
         group.barrier()
-        own_runs.append(t1 - t0)
-        runs.append(group.max(t1 - t0))
+        own_runs.append((t1 - t0) * 1e-9)
+        windows.append((t0, t1))
+        runs.append(group.max((t1 - t0) * 1e-9))
     elapsed = float(np.median(runs))
     total_pkts = world * args.steps * B
     value = total_pkts / elapsed / 1e6
     own_rate = args.steps * B / float(np.median(own_runs)) / 1e6
+    wstats = copdist.window_stats(group.gather_obj(windows), world, args.steps * B)
     log(f"[rank {rank}] {name}: timed {args.steps} steps x {len(runs)} runs ({engine}), median "
-        f"{elapsed * 1e3:.3f} ms -> {value:.1f} Mpkt/s (all ranks); runs {[round(x * 1e3, 3) for x in runs]} ms")
+        f"{elapsed * 1e3:.3f} ms -> {value:.1f} Mpkt/s (all ranks); runs {[round(x * 1e3, 3) for x in runs]} ms; "
+        f"windows overlap {wstats['windows_overlap']}, union {wstats['value_union']:.1f} Mpkt/s")
     res = {"W": W, "name": name, "B": B, "Lb": Lb, "P": P, "engine": engine, "value": value, "elapsed": elapsed,
-           "runs": runs, "own_rate": own_rate, "reduce_ms": reduce_ms, "rc_on": rc_on, "coll": coll, "fw_rules": fw_rules, "routes": routes,
+           "runs": runs, "own_rate": own_rate, "windows": wstats, "reduce_ms": reduce_ms, "rc_on": rc_on, "coll": coll,
+           "fw_rules": fw_rules, "routes": routes,
            "fw_tab": fw_tab, "rt_tab": rt_tab, "cnt_per_slot": cnt_per_slot, "d_pkts": d_pkts, "d_res": d_res,
            # every buffer the ring points at stays referenced as long as the
            # ring is used (a DeviceBuffer frees its memory when collected)
@@ -460,9 +475,18 @@ def measure(args, name, rank, world, dev, group, primary):
         r_ms = (time.perf_counter() - r0) * 1e3
         n_rules = len(ctx.rule_counters())
         want = [world * (args.warmup + args.steps) * B] + [world * args.steps * B] * (len(reduce_runs) - 1)
-        res["reduce_info"] = {"rccl_allreduce_u64_words": SHARD_AND_PORT_WORDS + n_rules,
+        per_iv = [round(group.max(x), 3) for x in res["reduce_ms"]]
+        med_red = float(np.median(per_iv)) if per_iv else 0.0
+        res["reduce_info"] = {"rccl_allreduce_u64_words": SHARD_AND_PORT_WORDS + n_rules, "ranks": world,
                               "ms": round(group.max(r_ms), 3),
-                              "ms_per_timed_interval": [round(group.max(x), 3) for x in res["reduce_ms"]],
+                              "ms_per_interval": per_iv,
+                              "timing": "each interval's reduce runs after its timed window, timed on its own "
+                                        "(max over ranks); value excludes it",
+                              "value_with_reduce_per_window": round(
+                                  world * args.steps * B / (res["elapsed"] + med_red * 1e-3) / 1e6, 3),
+                              "cadence": "reference: print_stats reads and zeroes every PRINT_DELAY = 2 s "
+                                         "(switch.h:23, switch.c:517-521); one reduce per 2 s costs "
+                                         f"{med_red / 2000.0 * 100:.4f} % of the interval",
                               "pkts_reduced_per_interval": reduce_runs,
                               "expected_per_interval": want, "ok": reduce_runs == want}
         if reduce_runs != want:
@@ -615,9 +639,18 @@ def main():
     ap.add_argument("--steps", type=int, default=16384)
     ap.add_argument("--warmup", type=int, default=2048)
     ap.add_argument("--workload", default="fw1k", choices=sorted(WORKLOADS))
-    ap.add_argument("--secondary", default="auto", choices=("auto", "none", "fw_lpm"),
-                    help="also time this workload in the same run (auto: fw_lpm, the north-star FW + LPM pipeline, "
-                         "when the primary is fw1k)")
+    ap.add_argument("--secondary", default="auto",
+                    help="also time these workloads in the same run, comma-separated, or none (auto, when the "
+                         "primary is fw1k: fw_lpm, the north-star FW + LPM pipeline (configs[3]); fw_lpm_imix "
+                         "(configs[2]); fw_lpm_1m, 1M + 1M tables with per-rule counters all-reduced over RCCL "
+                         "across every rank (configs[4]))")
+    ap.add_argument("--slots", default="static", choices=("static", "reuse", "always"),
+                    help="poll-mode slot declaration: static = the pool is written once before the start "
+                         "(COP_PMD_STATIC_SLOTS, no acquire); reuse = the default of cop_pmd_start (a system-scope "
+                         "acquire per tile once the ring wraps); always = an acquire on every tile")
+    ap.add_argument("--deadline", type=float, default=1500.0,
+                    help="seconds after which a rank that has not finished exits with status 124 (a hung rank "
+                         "must not hold the driver's node)")
     ap.add_argument("--per-launch", type=int, default=0,
                     help="batches per kernel launch (ring submit, at most 1024; 0: the workload's default). The "
                          "~23 us per-launch ramp and tail cost 6 %% at 384 batches, 2.5 %% at 1024")
@@ -655,12 +688,18 @@ def main():
     rank, world, local = copdist.env()
     secondary = args.secondary
     if secondary == "auto":
-        secondary = "fw_lpm" if args.workload == "fw1k" and not args.quick else "none"
+        secondary = "fw_lpm,fw_lpm_imix,fw_lpm_1m" if args.workload == "fw1k" and not args.quick else "none"
+    secondaries = [x for x in secondary.split(",") if x and x != "none" and x != args.workload]
+    bad = [x for x in secondaries if x not in WORKLOADS]
+    if bad:
+        raise SystemExit(f"[bench] unknown --secondary workload(s) {bad}: choose from {sorted(WORKLOADS)}")
     if args.quick:
         args.no_cpu = args.no_rccl_check = True
+    if args.deadline > 0:
+        watchdog(args.deadline, rank)
 
     if args.dry_run:
-        return dry_run(args, rank, world, local, WORKLOADS[args.workload])
+        return dry_run(args, rank, world, local, WORKLOADS[args.workload], secondaries)
     cg.lib()   # load the HIP runtime the product links (before torch)
     ndev = cg.device_count()
     check_devices(args, world, local, ndev)
@@ -669,8 +708,9 @@ def main():
     numa = copdist.bind_near_device(cg.device_pci_bus_id(dev)) if not no_bind else {"skipped": True}
     log(f"[rank {rank}] host side near device {dev}: {numa}")
     group = copdist.Group(rank, world, "gloo")
+    gate = copdist.StartGate(group)
 
-    res, ctx = measure(args, args.workload, rank, world, dev, group, primary=True)
+    res, ctx = measure(args, args.workload, rank, world, dev, group, gate, primary=True)
     W, B, P, Lb = res["W"], res["B"], res["P"], res["Lb"]
     ranks_info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(res["own_rate"], 3), "numa": numa,
                                    **({"rccl_init": res["coll"]} if res["rc_on"] else {})})
@@ -739,6 +779,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(res["elapsed"] * 1e3 / args.steps, 6),
         "runs_ms": [round(x * 1e3, 4) for x in res["runs"]],
+        # value = every rank's packets / the max over ranks of each rank's own
+        # window; beside it, how far the windows overlapped (the start gate
+        # opens them together) and the rate over their union
+        "windows_overlap": res["windows"]["windows_overlap"],
+        "value_union": round(res["windows"]["value_union"], 3),
+        "windows": res["windows"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -753,6 +799,7 @@ def main():
             "fw_rules": W["fw"],
             "route_prefixes": W["routes"],
             "route_form": args.route_form if W["routes"] else None,
+            "slots": args.slots if res["engine"] == "pmd" else None,
             "pkt_layout": "imix slab + u32 offsets" if W["imix"] else "64B slots",
             "stages": args.stages or W["stages"],
             "parallelism": f"independent per-GPU contexts x{world} (no data-path collective)",
@@ -802,21 +849,32 @@ def main():
         out["counter_allreduce_check"] = allreduce_check
     ctx.close()
 
-    # ---- the north-star workload (FW + LPM 100k, 64 B) in the same run ----
-    if secondary != "none":
+    # ---- the other BASELINE workloads in the same run: the north-star FW +
+    # LPM 100k (configs[3]), IMIX (configs[2]) and 1M + 1M with per-rule
+    # counters reduced over RCCL across every rank (configs[4]) ----
+    for sname in secondaries:
         try:
-            sres, sctx = measure(args, secondary, rank, world, dev, group, primary=False)
+            sres, sctx = measure(args, sname, rank, world, dev, group, gate, primary=False)
             sroof = roofline_block(sres, world, group, args)
-            out["secondary"] = {secondary: {
+            blk = {
                 "description": sres["W"]["desc"], "value": round(sres["value"], 3), "unit": "Mpkt/s",
                 "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(sres["elapsed"] * 1e3 / args.steps, 6),
                 "runs_ms": [round(x * 1e3, 4) for x in sres["runs"]], "engine": sres["engine"],
-                "route_form": args.route_form, "roofline": sroof}}
+                "windows_overlap": sres["windows"]["windows_overlap"],
+                "value_union": round(sres["windows"]["value_union"], 3),
+                "batch": sres["B"], "fw_rules": sres["W"]["fw"], "route_prefixes": sres["W"]["routes"],
+                "pkt_layout": "imix slab + u32 offsets" if sres["W"]["imix"] else "64B slots",
+                "route_form": args.route_form, "rule_counters": sres["rc_on"], "roofline": sroof}
+            if sres["rc_on"]:
+                blk["rccl_init"] = group.gather_obj(sres["coll"])
+            if "reduce_info" in sres:
+                blk["counter_reduce"] = sres["reduce_info"]
+            out.setdefault("secondary", {})[sname] = blk
             sctx.close()
         except Exception as e:  # noqa: BLE001 (the primary line stands)
-            out["secondary"] = {secondary: {"error": str(e)[:300]}}
-            log(f"[rank {rank}] secondary {secondary} failed: {e}")
+            out.setdefault("secondary", {})[sname] = {"error": str(e)[:300]}
+            log(f"[rank {rank}] secondary {sname} failed: {e}")
 
     # the CPU baseline: on rank 0 after the GPU timing, at
     # every N (north_star: "next to the reference DPDK CPU coprocessor timed
@@ -827,50 +885,96 @@ def main():
 
     if rank == 0:
         print(json.dumps(out), flush=True)
+    gate.close()
     group.close()
 
 
-def dry_run(args, rank, world, local, W):
+def watchdog(seconds: float, rank: int):
+    """End this rank with status 124 if it is still running after `seconds`
+    (a daemon timer: a rank stuck in a collective whose peer died must not
+    hold the node until the driver's own limit)."""
+    import threading
+
+    def fire():
+        log(f"[rank {rank}] deadline of {seconds:.0f} s passed: exiting (124)")
+        os._exit(124)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+
+
+def dry_run(args, rank, world, local, W, secondaries):
     """The launch/rank protocol with the GPU leg stubbed: device checks,
-    gloo rendezvous, the RCCL unique-id broadcast and the counter reduction
-    of rule-counter workloads (gloo sum standing in for the all-reduce, its
-    mismatch reported, not asserted), barrier-bracketed fake timings, max
-    over ranks, the per-rank gather and rank 0's one JSON line (CPU tests of
-    --gpus N)."""
+    gloo rendezvous, the start gate and its window stamps, the RCCL unique-id
+    broadcast and the counter reduction of rule-counter workloads (gloo sum
+    standing in for the all-reduce, its mismatch reported, not asserted),
+    fake timings, max over ranks, the per-rank gather, the secondary
+    workloads and rank 0's one JSON line (CPU tests of --gpus N). Inside
+    each window a rank sleeps its fake time: the windows' overlap is real."""
     if rank == args.dry_run_fail_rank:
         log(f"[rank {rank}] dry-run: failing on purpose")
         sys.exit(3)
     check_devices(args, world, local, args.dry_run_devices)
     dev = copdist.device_for(local, args.dry_run_devices)
     group = copdist.Group(rank, world, "gloo")
-    B = W["batch"]
-    rc_on = bool(W.get("rule_counters")) and not args.no_rule_counters
-    coll, reduce_info = None, None
-    if rc_on:
-        uid = group.broadcast_bytes(bytes(range(128)) if rank == 0 else None)
-        coll = "ok" if uid == bytes(range(128)) else "error: unique id differs"
-    runs, own, reduced = [], [], []
-    for r in range(max(1, args.repeats)):
-        group.barrier()
-        t = 1e-3 * (1.0 + 0.1 * rank)   # rank r "takes" (1 + r/10) ms per run
+    gate = copdist.StartGate(group)
+
+    def fake(name):
+        Wn = WORKLOADS[name]
+        B = Wn["batch"]
+        rc_on = bool(Wn.get("rule_counters")) and not args.no_rule_counters
+        coll, reduce_info = None, None
         if rc_on:
-            pk = (args.warmup if r == 0 else 0) + args.steps
-            reduced.append(int(group.sum_u64(np.array([pk * B], np.uint64))[0]))
-        own.append(t)
-        group.barrier()
-        runs.append(group.max(t))
-    if rc_on:
-        want = [world * (args.warmup + args.steps) * B] + [world * args.steps * B] * (len(reduced) - 1)
-        reduce_info = {"pkts_reduced_per_interval": reduced, "expected_per_interval": want, "ok": reduced == want}
-    elapsed = float(np.median(runs))
-    info = group.gather_obj({"rank": rank, "device": dev, "mpkt_s": round(args.steps * B / float(np.median(own)) / 1e6, 3),
-                             **({"rccl_init": coll} if rc_on else {})})
+            uid = group.broadcast_bytes(bytes(range(128)) if rank == 0 else None)
+            coll = "ok" if uid == bytes(range(128)) else "error: unique id differs"
+        runs, own, reduced, windows = [], [], [], []
+        for r in range(max(1, args.repeats)):
+            group.barrier()
+            t = 40e-3 * (1.0 + 0.01 * rank)   # rank r "takes" 40 (1 + r/100) ms per run
+            t0 = gate.open()
+            time.sleep(t)
+            t1 = copdist.monotonic_ns()
+            if rc_on:
+                pk = (args.warmup if r == 0 else 0) + args.steps
+                reduced.append(int(group.sum_u64(np.array([pk * B], np.uint64))[0]))
+            own.append(t)
+            windows.append((t0, t1))
+            group.barrier()
+            runs.append(group.max(t))
+        if rc_on:
+            want = [world * (args.warmup + args.steps) * B] + [world * args.steps * B] * (len(reduced) - 1)
+            reduce_info = {"ranks": world, "pkts_reduced_per_interval": reduced, "expected_per_interval": want,
+                           "ok": reduced == want}
+        elapsed = float(np.median(runs))
+        return {"B": B, "rc_on": rc_on, "coll": coll, "reduce_info": reduce_info, "own": own,
+                "value": world * args.steps * B / elapsed / 1e6,
+                "windows": copdist.window_stats(group.gather_obj(windows), world, args.steps * B)}
+
+    res = fake(args.workload)
+    info = group.gather_obj({"rank": rank, "device": dev,
+                             "mpkt_s": round(args.steps * res["B"] / float(np.median(res["own"])) / 1e6, 3),
+                             **({"rccl_init": res["coll"]} if res["rc_on"] else {})})
+    sec = {}
+    for sname in secondaries:
+        sr = fake(sname)
+        blk = {"value": round(sr["value"], 3), "windows_overlap": sr["windows"]["windows_overlap"],
+               "value_union": round(sr["windows"]["value_union"], 3), "batch": sr["B"],
+               "rule_counters": sr["rc_on"]}
+        if sr["rc_on"]:
+            blk["rccl_init"] = group.gather_obj(sr["coll"])
+            blk["counter_reduce"] = sr["reduce_info"]
+        sec[sname] = blk
     if rank == 0:
-        line = {"metric": METRIC, "value": round(world * args.steps * B / elapsed / 1e6, 3), "unit": "Mpkt/s",
+        line = {"metric": METRIC, "value": round(res["value"], 3), "unit": "Mpkt/s",
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                "windows_overlap": res["windows"]["windows_overlap"],
+                "value_union": round(res["windows"]["value_union"], 3), "windows": res["windows"],
                 "config": {"workload": args.workload, "ranks": info}}
-        if reduce_info:
-            line["counter_reduce"] = reduce_info
+        if res["reduce_info"]:
+            line["counter_reduce"] = res["reduce_info"]
+        if sec:
+            line["secondary"] = sec
         if not args.no_cpu:
             # the real CPU legs (oracle), on rank 0 at every N, as in a GPU run
             cid = W["cid"]
@@ -878,6 +982,7 @@ def dry_run(args, rank, world, local, W):
             line.update(cpu_legs(args, W, fw_rules))
         print(json.dumps(line), flush=True)
     group.barrier()
+    gate.close()
     group.close()
 
 

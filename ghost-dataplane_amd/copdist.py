@@ -14,6 +14,8 @@ the analogue of the reference's print_stats every PRINT_DELAY = 2 s
 from __future__ import annotations
 
 import os
+import tempfile
+import time
 
 import numpy as np
 
@@ -132,3 +134,101 @@ class Group:
     def close(self):
         if self._dist and self._dist.is_initialized():
             self._dist.destroy_process_group()
+
+
+def monotonic_ns() -> int:
+    """CLOCK_MONOTONIC: one clock for every process of the node, so the
+    ranks' window stamps compare directly."""
+    return time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+
+
+class StartGate:
+    """Opens every rank's timed window at one instant (the ranks of one node).
+
+    A gloo barrier releases its ranks one after another, and the skew can
+    exceed a 28 us window of the driver's 20 steps: each rank would then time
+    its own steps alone, and the max-over-ranks rate would claim N GPUs ran
+    at once when they never overlapped. The gate is one shared page in
+    /dev/shm (created by rank 0, its name broadcast over gloo, unlinked once
+    every rank has mapped it): per window, each rank stores its arm word and
+    spins on the release word; rank 0 waits until every rank is armed and
+    then stores the release. Every rank leaves the spin within a few hundred
+    ns of the store, then stamps CLOCK_MONOTONIC.
+
+    Layout: 64-byte lines of u64; line 0 the release sequence, line 1 + r
+    rank r's arm sequence."""
+
+    def __init__(self, group: "Group", timeout_s: float = 120.0):
+        import mmap
+        self.rank, self.world, self.timeout_s = group.rank, group.world, timeout_s
+        self.seq = 0
+        self._mm = self._w = None
+        if self.world == 1:
+            return
+        d = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+        size = 64 * (self.world + 1)
+        path = None
+        if self.rank == 0:
+            fd, path = tempfile.mkstemp(prefix="cop_gate_", dir=d)
+            os.ftruncate(fd, size)
+            os.close(fd)
+        path = group.broadcast_bytes(path.encode() if path else None).decode()
+        fd = os.open(path, os.O_RDWR)
+        try:
+            self._mm = mmap.mmap(fd, size)
+        finally:
+            os.close(fd)
+        group.barrier()   # every rank has it mapped: the name can go
+        if self.rank == 0:
+            os.unlink(path)
+        self._w = np.frombuffer(self._mm, dtype=np.uint64)
+
+    def _spin(self, ok, what):
+        t0 = time.monotonic()
+        while not ok():
+            if time.monotonic() - t0 > self.timeout_s:
+                raise TimeoutError(f"start gate: rank {self.rank} waited {self.timeout_s:.0f} s for {what}")
+
+    def open(self) -> int:
+        """Wait for every rank, open the window together; returns this
+        rank's window start (CLOCK_MONOTONIC ns)."""
+        self.seq += 1
+        if self._w is None:
+            return monotonic_ns()
+        w, s = self._w, np.uint64(self.seq)
+        w[8 * (1 + self.rank)] = s
+        if self.rank == 0:
+            self._spin(lambda: all(w[8 * (1 + r)] >= s for r in range(self.world)), "every rank to arm")
+            w[0] = s
+        else:
+            self._spin(lambda: w[0] >= s, "the release")
+        return monotonic_ns()
+
+    def close(self):
+        if self._mm is not None:
+            self._w = None
+            self._mm.close()
+            self._mm = None
+
+
+def window_stats(windows: list, world: int, pkts_per_rank: int) -> dict:
+    """windows[rank][run] = (t0_ns, t1_ns) of every rank's timed runs. Per
+    run: how far the ranks' windows overlap, as (min t1 - max t0) / the
+    ranks' median own time (1.0: all ran together; <= 0: never at once), the
+    start skew, and the rate over the union of the windows (every rank's
+    packets / (max t1 - min t0)): a value no rank's late or early start can
+    inflate. Medians over the runs beside the per-run lists."""
+    runs = len(windows[0])
+    overlap, skew_us, union = [], [], []
+    for k in range(runs):
+        t0 = [windows[r][k][0] for r in range(world)]
+        t1 = [windows[r][k][1] for r in range(world)]
+        own = float(np.median([t1[r] - t0[r] for r in range(world)]))
+        overlap.append(round((min(t1) - max(t0)) / own, 4) if own > 0 else 0.0)
+        skew_us.append(round((max(t0) - min(t0)) / 1e3, 2))
+        span = max(t1) - min(t0)
+        union.append(round(world * pkts_per_rank / (span * 1e-9) / 1e6, 3) if span > 0 else 0.0)
+    return {"start_gate": "shm" if world > 1 else "single rank", "clock": "CLOCK_MONOTONIC",
+            "windows_overlap": float(np.median(overlap)), "value_union": float(np.median(union)),
+            "start_skew_us_median": float(np.median(skew_us)),
+            "per_run": {"overlap": overlap, "start_skew_us": skew_us, "value_union": union}}

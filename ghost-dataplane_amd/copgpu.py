@@ -649,7 +649,8 @@ class Context:
 
 
 PMD_VARIABLE_N = 1
-PMD_SYS_ACQUIRE = 2
+PMD_SYS_ACQUIRE = 2     # acquire on every tile
+PMD_STATIC_SLOTS = 4    # slots written once before the start: no acquire (default: acquire once the ring wraps)
 
 
 class Pmd:

@@ -111,7 +111,7 @@ struct CopKParams {
     const uint32_t *lpm_tleaves;
     // bucketed form (COPK_TBL_BKT): lpm_bidx[b] = the last interval k with
     // start <= b << (32 - lpm_ib), b in [0, 2^lpm_ib] (the last entry: m - 1);
-    // lpm_bpairs[2k] = start k, [2k + 1] = its value (padded with four
+    // lpm_bpairs[2k] = start k, [2k + 1] = its value (padded with COP_BKT_PADS = 8
     // {0xFFFFFFFF, last value} pairs); lpm_lv lifting levels above the
     // widest bucket
     const uint32_t *lpm_bidx, *lpm_bpairs;
@@ -190,10 +190,18 @@ struct CopKPmd {
     uint32_t n_work;                     // worker workgroups
     uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
     uint32_t stepwise;                   // tiles step by step where tile_steps applies ($COP_PMD_STEPWISE=0: off)
-    uint32_t sys_acquire;                // rings in host memory: a system-scope acquire before each tile's loads
+    uint32_t sys_acquire;                // system-scope acquire before a tile's loads: 0 never (static slots),
+                                         // 1 every tile (host-memory rings), 2 once the ring wraps in this launch
     uint32_t test_skip;                  // tests: tile test_skip - 1 of ring 0's batch 0 never runs ($COP_PMD_TEST_SKIP_TILE)
     uint32_t poll_backoff;               // waiting workers' s_sleep(4) rounds between relay polls once idle
                                          // (3: ~0.3 us, the default; 0: busy polling, $COP_PMD_BACKOFF)
+    // dynamic tiles (segmented lists, step-by-step tiles): the ring's tiles
+    // are claimed from a ticket counter, tile T = seq0r[r] * tiles per batch
+    // + the T-th claim, instead of the static T = w + k * workers; a worker
+    // claims its next tile and issues that tile's header loads before it
+    // finishes the current one ($COP_PMD_DYN)
+    uint32_t dyn;
+    unsigned long long *d_ticket;        // device: ring r's claim counter at [16 r] (zeroed at every launch)
 };
 #define COPK_PMD_RELAYS 8
 #define COPK_PMD_GATE_SHIFT 56

@@ -324,12 +324,17 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                 lds_barrier();
             }
             const uint32_t ntiles = (n + TILE - 1) / TILE;
-            // Rings in host memory: the host rewrote the slot since this CU
-            // (or its XCD's L2) may last have read it, and a persistent
-            // kernel gets no dispatch-time cache invalidation, so each tile
-            // acquires at system scope before its loads (the doorbell read
-            // that made the batch visible came first).
-            if (P.sys_acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            // Slot reuse: another agent (the host, a copy engine, a NIC) may
+            // have rewritten the slot since this CU (or its XCD's L2) last
+            // read it, and a persistent kernel gets no dispatch-time cache
+            // invalidation, so the tile acquires at system scope before its
+            // loads (the doorbell read that made the batch visible came
+            // first). Mode 2 (the default): only from the ring's second lap
+            // in this launch on; a slot's first read in a launch follows the
+            // launch's own invalidation. Mode 1: every tile (host-memory
+            // rings, COP_PMD_SYS_ACQUIRE). Mode 0: never (COP_PMD_STATIC_SLOTS).
+            if (P.sys_acquire == 1u || (P.sys_acquire == 2u && b >= P.seq0r[r] + n_slots))
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             // The lane's index is made opaque each iteration, so the per-lane
             // values the tile derives from it (load geometry, LDS addresses) are
             // recomputed in the tile rather than hoisted out of the loop and held
@@ -380,10 +385,166 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             advance();
         }
     };
-    if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && p.rec_paired && P.stepwise)
-        serve(std::integral_constant<bool, steps_ok<FW, LPM, LAY, EXT>()>{});
-    else
+    // Dynamic tiles (P.dyn, step-by-step tiles only: segmented lists need no
+    // look-back, so any worker may take any tile and none ever waits on
+    // another). A worker claims tiles from its ring's ticket counter, one
+    // ahead: while it classifies and stores tile T, the header loads of its
+    // next tile Tn (claimed one tile earlier) are already in flight, and the
+    // claim of the tile after that too. Once T's stores, counter adds and
+    // those loads have drained (one vmcnt(0)), T is counted for its slot;
+    // that returning add is read one tile later (or before the worker waits
+    // for a post), so no round trip stands between two tiles. Workers the
+    // memory system serves first simply take more tiles: no static tail.
+    // Exits: a worker leaves only when its claimed tile's batch is at or
+    // above the closed gate's count; tickets are claimed in order, so every
+    // tile of every batch below the gate was claimed by a worker that serves
+    // it. A relaunch zeroes the tickets (ticket 0 = tile 0 of batch seq0r).
+    auto serve_dyn = [&](auto steps_c) {
+        // (two tiles' loads live at once: 256- and 512-packet tiles only)
+        constexpr bool STEPS = decltype(steps_c)::value && PPT <= 2;
+        if constexpr (STEPS) {
+            constexpr int W = COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT;
+            unsigned long long *ticket = P.d_ticket + (size_t)r * 16;
+            uint32_t *s_tk = lc.s_misc + 72;   // the next claimed ticket (lo, hi)
+            unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
+            const bool leader = wr % P.relay_stride == 0;
+            unsigned long long posted = 0;
+            // lane 0 of wave 0: the pending slot count (issued after a tile's
+            // stores drained, its return read one tile later)
+            unsigned long long pend_old = 0, pend_b = 0;
+            uint32_t pend_sl = 0;
+            bool pend = false;
+            auto pend_flush = [&] {
+                if (pend && (pend_old + 1) % tpb == 0)
+                    __hip_atomic_store(&P.h_done[rs0 + pend_sl], pend_b + 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                pend = false;
+            };
+            auto claim = [&] { return __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+            auto tk_get = [&] { return ((unsigned long long)s_tk[1] << 32) | s_tk[0]; };
+            // the first two claims
+            if (tid == 0) {
+                const unsigned long long t0 = claim();
+                const unsigned long long t1 = claim();
+                s_tk[0] = (uint32_t)t0;
+                s_tk[1] = (uint32_t)(t0 >> 32);
+                s_tk[2] = (uint32_t)t1;
+                s_tk[3] = (uint32_t)(t1 >> 32);
+            }
+            lds_barrier();
+            unsigned long long T = tk_get();
+            unsigned long long Tn = ((unsigned long long)s_tk[3] << 32) | s_tk[2];
+            lds_barrier();
+            // two load buffers used in turn (the loop body is instantiated
+            // once per buffer order): a tile's loads land in the registers
+            // its body reads, never in ones that must be copied (a copy of a
+            // register with a load in flight waits for the load)
+            u32x4 va[W][3], vb[W][3];
+            bool loaded = false;   // the current buffer holds tile T's header loads
+            uint32_t n = rg.n, ntiles = (rg.n + TILE - 1) / TILE;
+            const unsigned long long seq0 = P.seq0r[r];
+            // one tile: T's loads in cur (or issued here), Tn's into nxt;
+            // returns true when the worker is to leave
+            auto one = [&](u32x4 (&cur)[W][3], u32x4 (&nxt)[W][3]) -> bool {
+                int tid_i = tid;
+                asm volatile("" : "+v"(tid_i));
+                const int lane_i = tid_i & 63;
+                const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
+                const unsigned long long b = seq0 + T / tpb;
+                const uint32_t j = (uint32_t)(T % tpb);
+                const uint32_t slot = (uint32_t)(b % n_slots);
+                if (stamp && tid == 0) {
+                    st_stamp(&stamp[0], __builtin_amdgcn_s_memrealtime());   // diagnostic: tile start
+                    st_stamp(&stamp[4], b);
+                }
+                if (!loaded) {
+                    if (b >= posted) {
+                        // nothing posted for this tile yet: report the pending
+                        // count first (it may complete a batch), then wait
+                        if (tid == 0) {
+                            pend_flush();
+                            const unsigned long long hp = wait_posted(P, r, wr, b, leader);
+                            s_door[0] = (uint32_t)hp;
+                            s_door[1] = (uint32_t)(hp >> 32);
+                            s_door[2] = hp == 0 ? 1u : 0u;
+                        }
+                        lds_barrier();
+                        posted = ((unsigned long long)s_door[1] << 32) | s_door[0];
+                        const uint32_t leave = s_door[2];
+                        lds_barrier();
+                        if (leave) return true;
+                    }
+                    n = rg.n;
+                    if (P.h_n) {
+                        if (tid == 0)
+                            s_door[3] = __hip_atomic_load(&P.h_n[rs0 + slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        lds_barrier();
+                        n = min(s_door[3], rg.n);
+                        lds_barrier();
+                    }
+                    ntiles = (n + TILE - 1) / TILE;
+                    if (P.sys_acquire == 1u || (P.sys_acquire == 2u && b >= seq0 + n_slots))
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                    if (j < ntiles) steps_load<PPT, 0, W>(pmd_batch(p, rg, slot, n, ntiles), j, lane_i, wave_i, cur);
+                }
+                if (stamp && tid == 0) st_stamp(&stamp[1], __builtin_amdgcn_s_memrealtime());   // loads issued
+                // the next tile's loads, before this tile's work, when its
+                // batch is known posted (fixed-size batches)
+                const unsigned long long bn = seq0 + Tn / tpb;
+                const uint32_t jn = (uint32_t)(Tn % tpb);
+                const uint32_t sn = (uint32_t)(bn % n_slots);
+                const bool pf = bn < posted && !P.h_n;
+                if (pf) {
+                    if (P.sys_acquire == 1u || (P.sys_acquire == 2u && bn >= seq0 + n_slots))
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                    if (jn < ntiles) steps_load<PPT, 0, W>(pmd_batch(p, rg, sn, rg.n, ntiles), jn, lane_i, wave_i, nxt);
+                }
+                // and the claim after it
+                unsigned long long tnn = 0;
+                if (tid == 0) tnn = claim();
+                if (j < ntiles)
+                    tile_steps_v<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, pmd_batch(p, rg, slot, n, ntiles), j, tid_i,
+                                                                  lane_i, wave_i, cur);
+                if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done
+                // this tile's stores and counter adds landed (and the next
+                // tile's loads and the claim), then it is counted. The wait
+                // is the builtin, not inline asm: the compiler's wait
+                // insertion sees it, so it knows the claim's return (read by
+                // one lane below) has landed on every path and puts no
+                // vmcnt(0) after the next tile's loads
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched
+                asm volatile("" ::: "memory");
+                lds_barrier();
+                if (tid == 0) {
+                    pend_flush();
+                    pend_old = atomicAdd(&P.slot_tiles[(size_t)(rs0 + slot) * P.slot_stride], 1ull);
+                    pend_b = b;
+                    pend_sl = slot;
+                    pend = true;
+                    s_tk[0] = (uint32_t)tnn;
+                    s_tk[1] = (uint32_t)(tnn >> 32);
+                    if (stamp) st_stamp(&stamp[3], __builtin_amdgcn_s_memrealtime());   // counted
+                }
+                lds_barrier();
+                T = Tn;
+                Tn = tk_get();
+                loaded = pf;
+                return false;
+            };
+            for (;;) {
+                if (one(va, vb)) break;
+                if (one(vb, va)) break;
+            }
+            // leaving: the pending count was reported before the last wait
+        }
+    };
+    if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && p.rec_paired && P.stepwise) {
+        if (PPT <= 2 && P.dyn) serve_dyn(std::integral_constant<bool, steps_ok<FW, LPM, LAY, EXT>()>{});
+        else serve(std::integral_constant<bool, steps_ok<FW, LPM, LAY, EXT>()>{});
+    } else {
         serve(std::integral_constant<bool, false>{});
+    }
 }
 
 template <int FW, int LPM, int LAY, int PPT>
@@ -419,11 +580,15 @@ hipError_t pmd_lay(const CopKPmd *p, int lay, int ppt, int ext, uint32_t lds, hi
 template <int FW>
 hipError_t pmd_lpm(const CopKPmd *p, int lpm, int lay, int ppt, int ext, uint32_t lds, hipStream_t s, int *occ)
 {
+#ifdef COPK_ISA_PROBE   // ISA inspection builds only: one instantiation (tools/isa.sh)
+    return pmd_one<FW, COPK_TBL_OFF, COPK_LAY_COALESCED, COPK_ISA_PROBE>(p, ext, lds, s, occ);
+#else
     if (lpm == COPK_TBL_IVT) return pmd_lay<FW, COPK_TBL_IVT>(p, lay, ppt, ext, lds, s, occ);
     if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);
     if (lpm == COPK_TBL_TRIE) return pmd_lay<FW, COPK_TBL_TRIE>(p, lay, ppt, ext, lds, s, occ);
     if (lpm == COPK_TBL_BKT) return pmd_lay<FW, COPK_TBL_BKT>(p, lay, ppt, ext, lds, s, occ);
     return pmd_lay<FW, COPK_TBL_OFF>(p, lay, ppt, ext, lds, s, occ);
+#endif
 }
 
 }  // namespace

@@ -57,7 +57,7 @@ struct DevLpm {
     uint32_t t_nodes = 0, t_leaves = 0;
     // bucketed global form (COP_CFG_LPM_BKT; m == 0, ib / lv its own):
     // bidx = 2^ib + 1 first-candidate positions, bpairs = (start, value)
-    // pairs padded with four {0xFFFFFFFF, last value}; null if not built
+    // pairs padded with COP_BKT_PADS (8) {0xFFFFFFFF, last value}; null if not built
     uint32_t *bidx = nullptr, *bpairs = nullptr;
     uint32_t b_m = 0;
 };
@@ -1753,11 +1753,26 @@ int cop_coll_unique_id(uint8_t id[COP_COLL_ID_BYTES])
     return 0;
 }
 
+static int coll_init_free(cop_ctx *c, const uint8_t id[COP_COLL_ID_BYTES], int rank, int nranks);
+
 int cop_coll_init(cop_ctx *c, const uint8_t id[COP_COLL_ID_BYTES], int rank, int nranks)
 {
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return -EINVAL;
     if (!rccl_load()) return set_err(c, -ENOSYS, "librccl not available");
     HIPCHK(c, hipSetDevice(c->device));
+    // the communicator's set-up, its buffers (hipFree synchronises the
+    // device) and the prewarm all-reduce run with the GPU free, as every
+    // reduce does: a poll-mode kernel serving this context is paused around
+    // them (it holds every workgroup slot it could get)
+    if (int rc = pmd_pause(c)) return rc;
+    const int rc = coll_init_free(c, id, rank, nranks);
+    const int rrc = pmd_resume(c);
+    return rc ? rc : rrc;
+}
+
+// cop_coll_init with no poll-mode kernel on the GPU
+static int coll_init_free(cop_ctx *c, const uint8_t id[COP_COLL_ID_BYTES], int rank, int nranks)
+{
     coll_destroy(c);
     ncclUniqueId u;
     memcpy(u.internal, id, COP_COLL_ID_BYTES);
@@ -1996,7 +2011,8 @@ struct cop_pmd {
     uint8_t *dev = nullptr;                 // device words: ctl, gates, relays, slot tile counts, look-back
     size_t dev_bytes = 0;
     uint32_t n_rings = 1, n_slots = 0, tpb = 0, per_cu = 0, ring_n = 0;
-    bool sys_acquire = false;   // COP_PMD_SYS_ACQUIRE (host-memory rings get it regardless)
+    uint32_t acquire = 2;       // CopKPmd::sys_acquire: 2 on slot reuse (default), 1 every tile, 0 never
+    bool dyn = false;           // CopKPmd::dyn: dynamic tiles
     std::atomic<uint32_t> launches{0};
     uint32_t pauses = 0;                    // pmd_pause calls that stopped a running kernel
     bool was_live = false;                  // pmd_pause found it running (pmd_resume relaunches)
@@ -2018,12 +2034,14 @@ struct cop_pmd {
 // words, [576] the completion words, then the batch sizes (variable n)
 constexpr size_t PMD_H_STOP = 512, PMD_H_STATE = 516, PMD_H_DONE = 576;
 // device words: [8] d_ctl, [64] d_act, [1024 + 128 r] ring r's gate,
-// [2048 + 128 (8 r + x)] its relays, then the slot tile counts, then the
-// look-back chains (dense lists)
+// [2048 + 128 (8 r + x)] its relays, [PMD_TICKET_OFF + 128 r] its tile
+// ticket (dynamic tiles), then the slot tile counts, then the look-back
+// chains (dense lists)
 constexpr size_t PMD_ACT_OFF = 64;
 constexpr size_t PMD_GATE_OFF = 1024;
 constexpr size_t PMD_RELAY_OFF = 2048;
-constexpr size_t PMD_CTL_BYTES = PMD_RELAY_OFF + 128 * COPK_PMD_RELAYS * COPK_PMD_MAX_RINGS;
+constexpr size_t PMD_TICKET_OFF = PMD_RELAY_OFF + 128 * COPK_PMD_RELAYS * COPK_PMD_MAX_RINGS;   // dynamic tiles
+constexpr size_t PMD_CTL_BYTES = PMD_TICKET_OFF + 128 * COPK_PMD_MAX_RINGS;
 static_assert(PMD_GATE_OFF + 128 * COPK_PMD_MAX_RINGS <= PMD_RELAY_OFF, "gates overlap relays");
 static_assert(64 * COPK_PMD_MAX_RINGS <= PMD_H_STOP, "posted words overlap the stop word");
 
@@ -2078,16 +2096,24 @@ static int pmd_join(cop_pmd *m, double timeout_s)
     return 0;
 }
 
-// advance ring r's completed count over its completion words (the ring's thread)
+// advance ring r's completed count over its completion words. Any thread
+// may call it (the ring's own, a counter reader, cop_pmd_completed_ring):
+// the count only ever rises. A caller descheduled between its load and its
+// store must not move it back below a count the ring's thread has since
+// raised past a reposted slot: the scan from a lower count would stop at
+// that slot (its word then holds the newer sequence) for good.
 static uint64_t pmd_refresh(cop_pmd *m, uint32_t r)
 {
     PmdRing &g = m->ring[r];
     const uint64_t posted = g.posted.load(std::memory_order_relaxed);
-    uint64_t c = g.completed.load(std::memory_order_relaxed);
+    const uint64_t c0 = g.completed.load(std::memory_order_relaxed);
+    uint64_t c = c0;
     const volatile uint64_t *d = m->h_done + (size_t)r * m->n_slots;
     while (c < posted && d[c % m->n_slots] == c + 1) c++;
-    g.completed.store(c, std::memory_order_relaxed);
-    return c;
+    uint64_t cur = c0;
+    while (c > cur && !g.completed.compare_exchange_weak(cur, c, std::memory_order_relaxed)) {
+    }
+    return std::max(c, cur);
 }
 
 // count the binned rule hits of every completed batch not yet counted
@@ -2152,19 +2178,27 @@ static void pmd_size(cop_pmd *m)
     if (const char *e = getenv("COP_PMD_RELAY_STRIDE")) m->P.relay_stride = std::max(1u, (uint32_t)atoi(e));
     m->P.poll_backoff = 3;
     m->P.stepwise = getenv("COP_PMD_STEPWISE") && !atoi(getenv("COP_PMD_STEPWISE")) ? 0u : 1u;
+    m->P.dyn = m->dyn ? 1u : 0u;
     if (const char *e = getenv("COP_PMD_BACKOFF")) m->P.poll_backoff = std::min(64u, (uint32_t)atoi(e));
-    // rings whose packets live in host memory (mapped pinned: the drop-in's
-    // header records) are rewritten by the host between batches: a system-
-    // scope acquire before each tile's loads keeps the CU and L2 caches from
-    // serving a slot's previous batch
-    m->P.sys_acquire = m->sys_acquire ? 1u : 0u;
-    for (uint32_t q = 0; q < m->n_rings; q++) {
-        hipPointerAttribute_t at;
-        if (hipPointerGetAttributes(&at, m->P.rings[q].pkts) == hipSuccess && at.type == hipMemoryTypeHost)
-            m->P.sys_acquire = 1;
+    // Slot reuse (switch.c:463-470: the fast path refills the rings
+    // forever): a ring slot may be rewritten by another agent between its
+    // batches, and a persistent kernel gets no dispatch-time invalidation, so
+    // by default a tile acquires at system scope before its loads once its
+    // ring has wrapped in this launch (mode 2; a slot's first read in a
+    // launch is fresh). Rings whose packets live in host memory (mapped
+    // pinned: the drop-in's header records) acquire on every tile (mode 1,
+    // also COP_PMD_SYS_ACQUIRE); COP_PMD_STATIC_SLOTS declares the slots
+    // written once before the start (mode 0: no acquire).
+    m->P.sys_acquire = m->acquire;
+    if (m->acquire == 2u) {
+        for (uint32_t q = 0; q < m->n_rings; q++) {
+            hipPointerAttribute_t at;
+            if (hipPointerGetAttributes(&at, m->P.rings[q].pkts) == hipSuccess && at.type == hipMemoryTypeHost)
+                m->P.sys_acquire = 1;
+        }
+        (void)hipGetLastError();   // (an unregistered pointer leaves an error behind)
     }
-    (void)hipGetLastError();   // (an unregistered pointer leaves an error behind)
-    if (const char *e = getenv("COP_PMD_ACQUIRE")) m->P.sys_acquire = atoi(e) != 0;   // A/B runs
+    if (const char *e = getenv("COP_PMD_ACQUIRE")) m->P.sys_acquire = std::min(2u, (uint32_t)atoi(e));   // A/B runs
     // tests: a tile that never runs, so its successors' look-back gives up
     m->P.test_skip = getenv("COP_PMD_TEST_SKIP_TILE") ? (uint32_t)atoi(getenv("COP_PMD_TEST_SKIP_TILE")) + 1u : 0u;
 }
@@ -2308,7 +2342,10 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
     if (!c || !rings || !out || n_rings < 1) return -EINVAL;
     *out = nullptr;
     if (n_rings > COPK_PMD_MAX_RINGS) return set_err(c, -EINVAL, "pmd: %u rings > %d", n_rings, COPK_PMD_MAX_RINGS);
-    if (flags & ~(COP_PMD_VARIABLE_N | COP_PMD_SYS_ACQUIRE)) return set_err(c, -EINVAL, "pmd: unknown flags %#x", flags);
+    if (flags & ~(COP_PMD_VARIABLE_N | COP_PMD_SYS_ACQUIRE | COP_PMD_STATIC_SLOTS))
+        return set_err(c, -EINVAL, "pmd: unknown flags %#x", flags);
+    if ((flags & COP_PMD_SYS_ACQUIRE) && (flags & COP_PMD_STATIC_SLOTS))
+        return set_err(c, -EINVAL, "pmd: COP_PMD_SYS_ACQUIRE and COP_PMD_STATIC_SLOTS contradict");
     if (c->pmd) return set_err(c, -EBUSY, "this context already has a poll-mode kernel");
     const cop_batch_ring *r = &rings[0];
     for (uint32_t q = 0; q < n_rings; q++) {
@@ -2340,12 +2377,18 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
     m->c = c;
     m->n_rings = n_rings;
     m->ring_n = r->n;
-    m->sys_acquire = (flags & COP_PMD_SYS_ACQUIRE) != 0;
+    m->acquire = (flags & COP_PMD_SYS_ACQUIRE) ? 1u : (flags & COP_PMD_STATIC_SLOTS) ? 0u : 2u;
     Plan pl = plan_launch(c, (uint64_t)r->n * r->n_slots, imix, r->stride);
     // tile size: 1024-packet tiles (five workers per CU, so a 20-batch burst
     // of 64k packets is one tile per worker), 256-packet tiles for small
     // batches
     int ppt = r->n >= 4u * COPK_BLOCK * 4 ? 4 : 1;
+    // dynamic tiles ($COP_PMD_DYN=1; segmented lists, step-by-step tiles):
+    // claimed one ahead with the next tile's loads in flight, so 256-packet
+    // tiles (two tiles' loads in registers fit the 6-worker budget)
+    const char *dyn_env = getenv("COP_PMD_DYN");
+    m->dyn = dyn_env && atoi(dyn_env) != 0 && seg;
+    if (m->dyn) ppt = 1;
     if (c->ppt_override) ppt = c->ppt_override;
     pl.ppt = ppt;
     m->ppt = ppt;
@@ -2497,6 +2540,7 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
         m->P.d_act = (unsigned long long *)(m->dev + PMD_ACT_OFF);
         m->P.d_gate = (unsigned long long *)(m->dev + PMD_GATE_OFF);
         m->P.d_posted = (unsigned long long *)(m->dev + PMD_RELAY_OFF);
+        m->P.d_ticket = (unsigned long long *)(m->dev + PMD_TICKET_OFF);
         m->P.slot_tiles = (unsigned long long *)(m->dev + PMD_CTL_BYTES);
         p.look = look_words ? (unsigned long long *)(m->dev + look_off) : nullptr;
         p.err = nullptr;   // the look-back reports through d_ctl[2] (LookCtx)

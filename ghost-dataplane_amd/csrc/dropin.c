@@ -491,10 +491,11 @@ struct cop_pmd_host {
     cop_ctx *ctx;
     cop_pmd *pmd;
     uint32_t n_rings, n_slots, max_pkts;
-    uint8_t *h_stage;         /* [ring][slot][max_pkts] 16-byte header records (mapped) */
-    cop_result *h_res;        /* [ring][slot][max_pkts] result records (mapped) */
+    uint32_t slot_pkts;       /* max_pkts rounded up to even: the slot stride (16-byte aligned record slots) */
+    uint8_t *h_stage;         /* [ring][slot][slot_pkts] 16-byte header records (mapped) */
+    cop_result *h_res;        /* [ring][slot][slot_pkts] result records (mapped) */
     struct {
-        void **objs;          /* [slot][max_pkts] the mbufs each slot in flight holds */
+        void **objs;          /* [slot][slot_pkts] the mbufs each slot in flight holds */
         const void **data;    /* [max_pkts] the data addresses of one drain */
         uint32_t *n;          /* [slot] mbufs held */
         uint64_t head;        /* the ring's oldest batch in flight (its sequence number) */
@@ -526,25 +527,28 @@ int cop_pmd_host_create(cop_ctx *ctx, uint32_t n_rings, uint32_t max_pkts, uint3
     h->ctx = ctx;
     h->n_rings = n_rings;
     h->n_slots = n_slots;
-    h->max_pkts = max_pkts = (max_pkts + 1u) & ~1u;   /* even: 16-byte aligned record slots */
-    const size_t recs = (size_t)n_rings * n_slots * max_pkts;
+    /* the ring's batches hold at most max_pkts (<= max_batch); its slots are
+     * an even number of records apart (16-byte aligned record slots) */
+    h->max_pkts = max_pkts;
+    const uint32_t sp = h->slot_pkts = (max_pkts + 1u) & ~1u;
+    const size_t recs = (size_t)n_rings * n_slots * sp;
     void *d_stage = NULL, *d_res = NULL;
     int rc = cop_host_alloc_mapped(ctx, recs * COP_HDR16_STRIDE, (void **)&h->h_stage, &d_stage);
     if (!rc) rc = cop_host_alloc_mapped(ctx, recs * sizeof(cop_result), (void **)&h->h_res, &d_res);
     cop_batch_ring rings[COP_PMD_MAX_RINGS];
     for (uint32_t r = 0; !rc && r < n_rings; r++) {
-        h->ring[r].objs = (void **)calloc((size_t)n_slots * max_pkts, sizeof(void *));
+        h->ring[r].objs = (void **)calloc((size_t)n_slots * sp, sizeof(void *));
         h->ring[r].data = (const void **)calloc(max_pkts, sizeof(void *));
         h->ring[r].n = (uint32_t *)calloc(n_slots, sizeof(uint32_t));
         if (!h->ring[r].objs || !h->ring[r].data || !h->ring[r].n) rc = -ENOMEM;
         memset(&rings[r], 0, sizeof(rings[r]));
-        rings[r].pkts = (uint8_t *)d_stage + (size_t)r * n_slots * max_pkts * COP_HDR16_STRIDE;
+        rings[r].pkts = (uint8_t *)d_stage + (size_t)r * n_slots * sp * COP_HDR16_STRIDE;
         rings[r].n_slots = n_slots;
         rings[r].n = max_pkts;
         rings[r].stride = COP_HDR16_STRIDE;
-        rings[r].pkts_slot_bytes = (uint64_t)max_pkts * COP_HDR16_STRIDE;
-        rings[r].results = (cop_result *)d_res + (size_t)r * n_slots * max_pkts;
-        rings[r].results_slot = max_pkts;
+        rings[r].pkts_slot_bytes = (uint64_t)sp * COP_HDR16_STRIDE;
+        rings[r].results = (cop_result *)d_res + (size_t)r * n_slots * sp;
+        rings[r].results_slot = sp;
     }
     if (!rc) rc = cop_pmd_start_rings_stages(ctx, rings, n_rings, COP_PMD_VARIABLE_N, g_dropin_stages, &h->pmd);
     if (rc) {
@@ -561,7 +565,7 @@ static int pmd_host_complete(cop_pmd_host *h, uint32_t r, cop_ring *tx, cop_free
 {
     const uint64_t b = h->ring[r].head;
     const uint32_t slot = (uint32_t)(b % h->n_slots);
-    void **objs = h->ring[r].objs + (size_t)slot * h->max_pkts;
+    void **objs = h->ring[r].objs + (size_t)slot * h->slot_pkts;
     const uint32_t n = h->ring[r].n[slot];
     const int prof = prof_on();
     uint64_t t0 = prof ? prof_ns() : 0;
@@ -577,7 +581,7 @@ static int pmd_host_complete(cop_pmd_host *h, uint32_t r, cop_ring *tx, cop_free
         drop_all(objs, n, free_fn, free_arg, stats);   /* no verdicts: freed, never leaked */
         return rc;
     }
-    const cop_result *res = h->h_res + ((size_t)r * h->n_slots + slot) * h->max_pkts;
+    const cop_result *res = h->h_res + ((size_t)r * h->n_slots + slot) * h->slot_pkts;
     forward_batch(tx, objs, res, n, free_fn, free_arg, stats);
     if (prof) {
         tl_prof[PROF_FWD] += prof_ns() - t0;
@@ -601,7 +605,7 @@ int cop_coprocessor_poll_pmd(cop_pmd_host *h, uint32_t r, cop_ring *rx, cop_ring
         done += c;
     }
     const uint32_t slot = (uint32_t)(posted % h->n_slots);
-    void **objs = h->ring[r].objs + (size_t)slot * h->max_pkts;
+    void **objs = h->ring[r].objs + (size_t)slot * h->slot_pkts;
     const int prof = prof_on();
     uint64_t t0 = prof ? prof_ns() : 0;
     const uint32_t n = drain_rx(rx, objs, h->ring[r].data, max_pkts);
@@ -614,7 +618,7 @@ int cop_coprocessor_poll_pmd(cop_pmd_host *h, uint32_t r, cop_ring *rx, cop_ring
     }
     if (n) {
         cop_pack_headers(h->ring[r].data, n,
-                         h->h_stage + (((size_t)r * h->n_slots + slot) * h->max_pkts) * COP_HDR16_STRIDE);
+                         h->h_stage + (((size_t)r * h->n_slots + slot) * h->slot_pkts) * COP_HDR16_STRIDE);
         int rc = cop_pmd_post_batch(h->pmd, r, n);
         if (rc) {
             drop_all(objs, n, free_fn, free_arg, stats);

@@ -442,12 +442,21 @@ int cop_pmd_stop(cop_pmd *pmd);
  * COP_PMD_MAX_RINGS. The single-ring calls above act on ring 0. */
 #define COP_PMD_MAX_RINGS 8
 #define COP_PMD_VARIABLE_N 1u   /* batches carry their own packet count (cop_pmd_post_batch) */
-/* Each tile acquires at system scope before it loads its packets: for rings
- * whose slots another agent (the host, a NIC, another GPU) rewrites between
- * batches. A persistent kernel gets no dispatch-time cache invalidation, so
- * without it a CU or L2 may serve a slot's previous contents. Rings in host
- * memory get it without the flag. */
+/* Slot reuse. The reference's fast path refills its rings forever
+ * (switch.c:463-470), and a ring slot here may likewise be rewritten by
+ * another agent (the host with cop_memcpy_h2d, a NIC, another GPU) between
+ * its batches. A persistent kernel gets no dispatch-time cache invalidation,
+ * so a CU or L2 could serve a slot's previous contents. By DEFAULT (no flag,
+ * and always through cop_pmd_start) every tile acquires at system scope
+ * before it loads its packets once its ring has wrapped in the running
+ * launch: a slot's first read in a launch is fresh, every reuse is safe.
+ * COP_PMD_SYS_ACQUIRE: acquire on every tile (rings in host memory get this
+ * without the flag). COP_PMD_STATIC_SLOTS: the caller declares the slots
+ * written once before cop_pmd_start_rings and never again while the kernel
+ * runs (a benchmark's resident pool): no acquire. The two contradict
+ * (-EINVAL). */
 #define COP_PMD_SYS_ACQUIRE 2u
+#define COP_PMD_STATIC_SLOTS 4u
 int cop_pmd_start_rings(cop_ctx *ctx, const cop_batch_ring *rings, uint32_t n_rings, uint32_t flags,
                         cop_pmd **out);
 /* Post the next `count` full batches (n packets each) of one ring. */

@@ -33,9 +33,12 @@ def test_spawn_two_ranks_one_line():
     ranks = j["config"]["ranks"]
     assert [x["rank"] for x in ranks] == [0, 1]
     assert sorted(x["device"] for x in ranks) == [0, 1]          # one device per rank
-    # max over ranks: rank 1 "takes" 1.1 ms, so the job rate is 2 x its rate
+    # max over ranks: rank 1 "takes" 40.4 ms, so the job rate is 2 x its rate
     b = 65536
-    assert abs(j["value"] - 2 * 20 * b / 1.1e-3 / 1e6) < 1e-3 * j["value"]
+    assert abs(j["value"] - 2 * 20 * b / 40.4e-3 / 1e6) < 1e-3 * j["value"]
+    # the start gate opened both windows together
+    assert j["windows"]["start_gate"] == "shm" and j["windows_overlap"] >= 0.9
+    assert 0 < j["value_union"] <= 2 * 20 * b / 40e-3 / 1e6 * 1.001
     assert ranks[0]["mpkt_s"] > ranks[1]["mpkt_s"]
     # the CPU baseline rides every N's line (N > 1 lines had none)
     cb = j["cpu_baseline"]
@@ -93,3 +96,44 @@ def test_failing_rank_ends_the_others_fast():
     assert r.returncode != 0
     assert _t.time() - t0 < 60
     assert "failed first" in r.stderr
+
+
+def test_eight_ranks_gate_overlap_and_config5_block():
+    """The driver's 8-GPU command: 8 ranks, the shared-memory start gate
+    opens every rank's window at once (each rank sleeps its fake time inside
+    it, so the overlap is measured, not assumed): windows_overlap >= 0.9 and
+    the union-window rate beside the max-own value; the configs[4] secondary
+    (fw_lpm_1m: 1M + 1M, 256k batches, per-rule counters reduced over all
+    ranks) rides the line with its reduction checked across 8 ranks."""
+    r = run("--gpus", "8", "--dry-run", "--steps", "20", "--warmup", "5", "--repeats", "5", "--no-cpu",
+            timeout=600)
+    assert r.returncode == 0, r.stderr
+    lines = json_lines(r.stdout)
+    assert len(lines) == 1
+    j = lines[0]
+    assert j["n_gpus"] == 8 and len(j["config"]["ranks"]) == 8
+    assert j["windows_overlap"] >= 0.9, j["windows"]
+    assert len(j["windows"]["per_run"]["overlap"]) == 5
+    b = 65536
+    # value: max over ranks (rank 7 takes 42.8 ms); union: never above every
+    # rank running its packets in the fastest rank's time
+    assert abs(j["value"] - 8 * 20 * b / 42.8e-3 / 1e6) < 1e-3 * j["value"]
+    assert j["value_union"] <= 8 * 20 * b / 40e-3 / 1e6 * 1.001
+    c5 = j["secondary"]["fw_lpm_1m"]
+    assert c5["rule_counters"] and c5["rccl_init"] == ["ok"] * 8
+    B = 262144
+    assert c5["counter_reduce"]["ok"] and c5["counter_reduce"]["ranks"] == 8
+    assert c5["counter_reduce"]["pkts_reduced_per_interval"] == [8 * 25 * B] + [8 * 20 * B] * 4
+    assert c5["windows_overlap"] >= 0.9
+    assert {"fw_lpm", "fw_lpm_imix", "fw_lpm_1m"} <= set(j["secondary"])
+
+
+def test_start_gate_and_window_stats_in_process():
+    """window_stats on hand-made windows: overlap, skew and the union rate."""
+    import copdist
+    w = [[(0, 1000)], [(100, 1100)]]          # two ranks, 100 ns apart, 1000 ns each
+    st = copdist.window_stats(w, 2, 10)
+    assert st["windows_overlap"] == 0.9 and st["start_skew_us_median"] == 0.1
+    assert abs(st["value_union"] - 2 * 10 / 1100e-9 / 1e6) < 1e-3   # (rounded to 3 decimals)
+    w = [[(0, 1000)], [(2000, 3000)]]         # windows that never met
+    assert copdist.window_stats(w, 2, 10)["windows_overlap"] < 0

@@ -200,12 +200,16 @@ def test_hdr16_rings_variable_n(gpu_ctx_factory, stages):
                 assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"ring {r} batch {i} (n={n})"
 
 
-def test_slots_rewritten_between_batches(gpu_ctx_factory):
+@pytest.mark.parametrize("flags", [cg.PMD_SYS_ACQUIRE, 0])
+def test_slots_rewritten_between_batches(gpu_ctx_factory, flags):
     """A producer that rewrites ring slots between batches (here the host,
-    by copies into HBM; on a real deployment a NIC): with COP_PMD_SYS_ACQUIRE
-    each tile acquires before its loads, so a slot's new packets are read,
-    never the previous batch's that a CU or L2 may still hold. Eight
-    generations through a two-slot ring, records and lists per batch."""
+    by cop_memcpy_h2d copies into HBM; on a real deployment a NIC, as the
+    reference's fast path refills its rings, switch.c:463-470): each tile
+    acquires before its loads once the ring has wrapped (the default: flags
+    0 goes through the single-ring cop_pmd_start) or on every tile
+    (COP_PMD_SYS_ACQUIRE), so a slot's new packets are read, never the
+    previous batch's that a CU or L2 may still hold. Eight generations
+    through a two-slot ring, records and lists per batch."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
@@ -213,7 +217,7 @@ def test_slots_rewritten_between_batches(gpu_ctx_factory):
     B, P = 65536, 2
     gens = [cg.gen_trace(0x5EED7500 + g, B, rules) for g in range(8)]
     rg = SegRing(ctx, np.concatenate([gens[0], gens[1]]), B, P)
-    with ctx.pmd_start(rg.ring, cg.PMD_SYS_ACQUIRE) as m:
+    with ctx.pmd_start(rg.ring, flags) as m:
         for g in range(8):
             s_ = g % P
             if g >= P:
@@ -227,3 +231,136 @@ def test_slots_rewritten_between_batches(gpu_ctx_factory):
             assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"generation {g}"
             assert np.array_equal(seg_to_dense(fwd, cnt, B), fo), f"generation {g} list"
         assert m.info()["launches"] == 1   # served by one launch: no relaunch invalidated the caches
+
+
+def test_static_slots_contradicts_acquire(gpu_ctx_factory):
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    rg = SegRing(ctx, cg.gen_trace(0x5EED7510, 2 * 65536, rules), 65536, 2)
+    with pytest.raises(cg.CopError):
+        ctx.pmd_start(rg.ring, cg.PMD_SYS_ACQUIRE | cg.PMD_STATIC_SLOTS)
+    with ctx.pmd_start(rg.ring, cg.PMD_STATIC_SLOTS) as m:   # the bench's declaration
+        m.run(4)
+    assert ctx.counters()["rx"] == 4 * 65536
+
+
+def fw_hits_per_slot(pk, B, P, fw):
+    """FW hits (records with the FW-hit flag) of each slot's batch."""
+    out = []
+    for s_ in range(P):
+        r, _ = oracle_batch(pk[s_ * B * 64:(s_ + 1) * B * 64], B, S | F, fw)
+        out.append(int(((r["flags"] & 2) != 0).sum()))
+    return out
+
+
+@pytest.mark.parametrize("rule_counters", [False, True])
+def test_pause_while_rings_post_from_threads(gpu_ctx_factory, rule_counters):
+    """every counter read pauses the poll-mode kernel (it finishes
+    the batches below its gates, leaves, and is relaunched from each ring's
+    first incomplete batch). Four rings posted and waited by four threads
+    while a fifth thread reads the counters (and, with per-rule counters,
+    reads and zeroes them) in a loop, so pauses land while other threads have
+    batches in flight and while they post: every ring's records and lists
+    stay bit-exact, the packet count and the per-rule hit totals are exact
+    (each batch counted once), and the kernel was relaunched."""
+    rules = fw1k()
+    flags = cg.CFG_SEG_LISTS | (cg.CFG_RULE_COUNTERS if rule_counters else 0)
+    ctx = gpu_ctx_factory(stages=S | F, flags=flags)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    fw, _ = oracle_tables(rules)
+    B, P, R = 65536, 4, 4
+    pks = [cg.gen_trace(0x5EED7600 + r, B * P, rules) for r in range(R)]
+    rgs = [SegRing(ctx, pk, B, P) for pk in pks]
+    posted = [0] * R
+    stop = threading.Event()
+    reads = [0]
+    hits_read = [0]
+    seen_rx = []
+    m = ctx.pmd_start([g.ring for g in rgs])
+
+    def reader():
+        while not stop.is_set():
+            seen_rx.append(ctx.counters()["rx"])
+            if rule_counters:
+                hits_read[0] += int(ctx.rule_counters(reset=True).sum())
+            reads[0] += 1
+
+    def feeder(r):
+        def f():
+            for i in range(24):
+                k = 1 + (i + r) % 3
+                m.post_ring(r, k)
+                posted[r] += k
+                if i % 4 == 3:
+                    m.wait_ring(r)
+            m.wait_ring(r)
+        return f
+
+    rd = threading.Thread(target=reader)
+    rd.start()
+    try:
+        run_threads([feeder(r) for r in range(R)])
+    finally:
+        stop.set()
+        rd.join(120)
+    assert not rd.is_alive(), "the counter reader hung"
+    launches = m.info()["launches"]
+    m.stop()
+    for r in range(R):
+        rgs[r].check(pks[r], S | F, fw)
+    assert ctx.counters()["rx"] == sum(posted) * B
+    assert seen_rx == sorted(seen_rx)                       # counts never go back
+    assert reads[0] >= 2 and launches >= 2, (reads[0], launches)
+    if rule_counters:
+        per_slot = [fw_hits_per_slot(pks[r], B, P, fw) for r in range(R)]
+        want = sum(per_slot[r][b % P] for r in range(R) for b in range(posted[r]))
+        assert hits_read[0] + int(ctx.rule_counters().sum()) == want
+
+
+def test_completed_count_never_moves_back(gpu_ctx_factory):
+    """a ring's completed count is read and raised by threads
+    other than the ring's own (cop_pmd_completed_ring, and the binned-hit
+    flush of cop_rule_counters_read for ring 0). One thread posts a 4-slot
+    ring one batch at a time far past its slots while another calls both in
+    a loop: the count it sees never falls, the poster never stalls on a
+    count moved back below a reposted slot, and the hits are exact."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS | cg.CFG_RULE_COUNTERS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    fw, _ = oracle_tables(rules)
+    B, P, N = 65536, 4, 96
+    pk = cg.gen_trace(0x5EED7700, B * P, rules)
+    rg = SegRing(ctx, pk, B, P)
+    stop = threading.Event()
+    seen = []
+    m = ctx.pmd_start(rg.ring)
+
+    def watcher():
+        while not stop.is_set():
+            seen.append(m.completed_ring(0))
+            ctx.rule_counters()
+            time.sleep(0)
+
+    def poster():
+        for i in range(N):
+            m.post(1)
+            if i % 8 == 7:
+                m.wait()
+        m.wait()
+
+    w = threading.Thread(target=watcher)
+    w.start()
+    try:
+        t0 = time.time()
+        run_threads([poster])
+        assert time.time() - t0 < 60
+    finally:
+        stop.set()
+        w.join(120)
+    assert not w.is_alive()
+    assert seen == sorted(seen) and seen[-1] <= N
+    m.stop()
+    rg.check(pk, S | F, fw)
+    per_slot = fw_hits_per_slot(pk, B, P, fw)
+    assert int(ctx.rule_counters().sum()) == sum(per_slot[b % P] for b in range(N))

@@ -101,3 +101,48 @@ def test_large_table_all_addresses_of_a_dense_chunk(gpu_ctx_factory, mode, monke
     ro, fo, _ = orc.process(pk, n, stages=S | L, route=ort)
     rg, fg, _ = gpu_run(ctx, pk, n)
     assert_parity(rg, fg, ro, fo)
+
+
+def test_bkt_wide_bucket_on_device(gpu_ctx_factory):
+    """The bucketed form's wide-bucket scan (bkt_step's ballot rounds for a
+    bucket with more than 7 boundaries) run by the GPU kernels, not only by
+    the host mirror: 100 host routes inside one /24 among 30k
+    random routes (so the table leaves LDS for CFG_LPM_BKT); every address of
+    that /24 and of its neighbours, through a one-shot launch and through the
+    poll-mode kernel, against the oracle."""
+    dense = np.zeros(100, dtype=cg.PREFIX_DT)
+    dense["ip"] = 0x0A0B0C00 + 2 * np.arange(100, dtype=np.uint32)
+    dense["depth"] = 32
+    dense["next_hop"] = 100 + np.arange(100)
+    routes = np.concatenate([cg.gen_rules(0x5EED2098, 30000, cg.GEN_ROUTES, 0), dense])
+    rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
+    assert len(rtt.intervals()[0]) > 8192
+    ips = np.arange(0x0A0B0B00, 0x0A0B0E00, dtype=np.uint32)          # the /24 and both neighbours
+    _, _, info = rtt.bkt_probe(ips, 0)
+    assert info["lifted"] > 0, info                                    # the wide-bucket scan is reached
+    ort = orc.OracleLpm(1 << 20, 1 << 16)
+    ort.setup(routes["ip"], routes["depth"], routes["next_hop"], stop_at_error=False)
+    n = 65536
+    pk = cg.gen_trace(0x5EED0079, n, None, routes, opts=cg.trace_opts(pct_non_ipv4=0))
+    pk2 = pk.reshape(n, 64)
+    d = ips[np.arange(n) % len(ips)]
+    pk2[:, 30:34] = d.astype(">u4").view(np.uint8).reshape(-1, 4)
+    ro, fo, _ = orc.process(pk, n, stages=S | L, route=ort)
+    assert ((ro["flags"] & 1) == 1).mean() > 0.3
+    ctx = gpu_ctx_factory(stages=S | L, flags=cg.CFG_LPM_BKT | cg.CFG_SEG_LISTS)
+    ctx.set_route_lpm(rtt)
+    assert ctx.route_form() == "bkt"
+    rg, _, _ = gpu_run(ctx, pk, n, compact=False)
+    for f in ("verdict", "flags", "port", "route_nh"):
+        assert np.array_equal(rg[f], ro[f]), f"one-shot {f}"
+    # the poll-mode kernel (its own instantiation of the bkt lookup)
+    dp = ctx.alloc(pk.nbytes)
+    dp.upload(pk)
+    dr = ctx.alloc(n * 8)
+    dr.fill(0xEE)
+    ring = cg.make_ring(dp, 1, n, dr, n * 64)
+    with ctx.pmd_start(ring) as m:
+        m.run(3)
+    res = dr.download(cg.RESULT_DT, n)
+    for f in ("verdict", "flags", "port", "route_nh"):
+        assert np.array_equal(res[f], ro[f]), f"poll mode {f}"

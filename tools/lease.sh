@@ -1,0 +1,100 @@
+#!/bin/bash
+# One GPU lease: named steps, in order, each under its own time limit
+# (tools/gpu_step.sh: a fault-like exit ends the call there).
+#
+# usage (through gpurun, from the repo root):
+#   bash tools/lease.sh <out> <step> [<step> ...]
+# <out>: directory under gpurun_out/ for the logs (e.g. r05/check1).
+# Steps:
+#   pytest          every -m gpu test (one process)
+#   pytest:<expr>   the -m gpu tests matching -k <expr>
+#   smoke           __graft_entry__.smoke()
+#   bench20         the driver's command: bench.py --gpus 1 --steps 20 --warmup 5
+#   bench_default   bench.py with no flags
+#   slots           the driver's command at --slots static / reuse / always (quick, 11 runs each)
+#   stats20         rocprofv3 --kernel-trace --stats of the driver's command
+#   pmc_pmd         FETCH_SIZE / WRITE_SIZE passes over a 1024-batch poll-mode post + membench calibration
+#   c5              config 5 (fw_lpm_1m) at 20 steps, quick, route form $C5_FORM (dir)
+#   c5_forms        config 5 in every FW x route form: dir/dir, dir/bkt, bkt/bkt (quick)
+#   imix            FW + LPM 100k IMIX at 20 steps (quick)
+#   rings           the ring loops (tools/ringbench: 1 and 5 loops, sync / async / pmd)
+#   probe           tools/pmd_probe.py stamps of the 20-batch post
+# Extra arguments for bench steps: $BENCH_ARGS.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+out=$R/gpurun_out/$1
+shift
+mkdir -p "$out"
+export TMPDIR=/tmp
+step() { "$R/tools/gpu_step.sh" "$@" || exit 99; }
+line() { grep -h '^{"metric"' "$@" | cut -c1-400; }
+B="python3 -u $R/bench.py"
+for s in "$@"; do
+  case $s in
+    pytest)
+      step 900 "$out/pytest.log" python3 -u -m pytest "$R/tests" -m gpu -v --timeout 120 --timeout-method thread
+      grep -E "FAILED|ERROR|passed|failed" "$out/pytest.log" | tail -6 ;;
+    pytest:*)
+      k=${s#pytest:}
+      step 600 "$out/pytest_${k//[^A-Za-z0-9_]/_}.log" python3 -u -m pytest "$R/tests" -m gpu -v -k "$k" --timeout 120 --timeout-method thread
+      grep -E "FAILED|ERROR|passed|failed" "$out/pytest_${k//[^A-Za-z0-9_]/_}.log" | tail -6 ;;
+    smoke)
+      step 300 "$out/smoke.log" python3 -u -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
+    bench20)
+      step 600 "$out/bench20.log" $B --gpus 1 --steps 20 --warmup 5 $BENCH_ARGS
+      line "$out/bench20.log" ;;
+    bench_default)
+      step 600 "$out/bench_default.log" $B $BENCH_ARGS
+      line "$out/bench_default.log" ;;
+    slots)
+      for v in static reuse always static reuse always; do
+        step 200 "$out/slots_$v.log" $B --quick --steps 20 --warmup 5 --repeats 11 --slots $v $BENCH_ARGS
+        echo "$v $(line "$out/slots_$v.log" | cut -c1-200)"
+      done ;;
+    stats20)
+      step 300 "$out/stats20.log" rocprofv3 --kernel-trace --stats -d "$out/stats20" -o bench --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu $BENCH_ARGS ;;
+    pmc_pmd)
+      step 200 "$out/pmd_pmc_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/pmd_fetch" -o pmd --output-format csv -- python3 "$R/tools/pmc_pmd.py" run --batches 1024
+      step 200 "$out/pmd_pmc_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/pmd_write" -o pmd --output-format csv -- python3 "$R/tools/pmc_pmd.py" run --batches 1024
+      step 200 "$out/mb_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/mb_fetch" -o mb --output-format csv -- "$R/tools/membench"
+      step 200 "$out/mb_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/mb_write" -o mb --output-format csv -- "$R/tools/membench" ;;
+    c5)
+      step 300 "$out/c5_${C5_FORM:-dir}.log" $B --quick --workload fw_lpm_1m --steps 20 --warmup 5 --route-form "${C5_FORM:-dir}" $BENCH_ARGS
+      line "$out/c5_${C5_FORM:-dir}.log" ;;
+    c5_forms)
+      for f in "dir dir" "dir bkt" "bkt bkt"; do
+        set -- $f
+        COP_FW_FORM=$1 step 300 "$out/c5_fw$1_rt$2.log" $B --quick --workload fw_lpm_1m --steps 20 --warmup 5 --route-form "$2" $BENCH_ARGS
+        echo "fw $1 route $2: $(line "$out/c5_fw$1_rt$2.log" | cut -c1-200)"
+      done ;;
+    imix)
+      step 300 "$out/imix20.log" $B --quick --workload fw_lpm_imix --steps 20 --warmup 5 $BENCH_ARGS
+      line "$out/imix20.log" ;;
+    rings)
+      for m in sync async pmd; do
+        a=""; [ $m != sync ] && a=$m
+        COP_HOST_PROF=1 step 90 "$out/ring1_$m.log" "$R/tools/ringbench" 8388608 16384 1 $a
+        COP_HOST_PROF=1 step 120 "$out/ring5_$m.log" "$R/tools/ringbench" 8388608 16384 5 $a
+      done
+      grep -h "aggregate" "$out"/ring*.log ;;
+    dyn)
+      # dynamic tiles ($COP_PMD_DYN=1) against the static order, alternating
+      i=0
+      for v in 0 1 0 1; do
+        i=$((i + 1))
+        COP_PMD_DYN=$v step 300 "$out/dyn${v}_$i.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS
+        grep -h '^{"metric"' "$out/dyn${v}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("dyn", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$v"
+      done
+      for v in 0 1; do
+        COP_PMD_DYN=$v step 300 "$out/dyn_steady$v.log" python3 -u "$R/tools/pmd_probe.py"
+      done ;;
+    pytest_dyn)
+      COP_PMD_DYN=1 step 600 "$out/pytest_dyn.log" python3 -u -m pytest "$R/tests" -m gpu -v -k "pmd or seg or rings or dropin" --timeout 120 --timeout-method thread
+      grep -E "FAILED|ERROR|passed|failed" "$out/pytest_dyn.log" | tail -6 ;;
+    probe)
+      step 200 "$out/probe.log" python3 -u "$R/tools/pmd_probe.py" ;;
+    *)
+      echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo done
