@@ -191,7 +191,7 @@ def check_devices(args, world, local, ndev):
                          f"own GPU (--allow-shared-gpu to time ranks sharing GPUs anyway)")
 
 
-def table_probes(fw_tab, rt_tab, sample, imix_offsets, route_form):
+def table_probes(fw_tab, rt_tab, sample, imix_offsets, route_form, fw_form="dir"):
     """SURVEY.md §8(d): LPM table probes are not in the algorithmic bytes;
     report them per packet, from a sample batch of the workload (host-side
     restatement of which packets reach each stage). LDS forms issue no
@@ -209,7 +209,7 @@ def table_probes(fw_tab, rt_tab, sample, imix_offsets, route_form):
     reach = (et == 0x0800) & ((dst & 0xFFFF) > 4)   # stage P: the default routing table's UNKNOWN entries
     n = len(hdr)
     out = {"sample_pkts": int(n), "reach_stage_p": round(float(reach.mean()), 4)}
-    for name, tab, key, form in (("fw", fw_tab, src, "dir"), ("route", rt_tab, dst, route_form)):
+    for name, tab, key, form in (("fw", fw_tab, src, fw_form), ("route", rt_tab, dst, route_form)):
         if tab is None:
             continue
         if len(tab.intervals()[0]) <= 8192:
@@ -221,7 +221,7 @@ def table_probes(fw_tab, rt_tab, sample, imix_offsets, route_form):
         if form == "bkt":
             # one 8-byte index load + one 16-byte pair load per reaching
             # packet, plus the wide-bucket rounds (two 16-byte loads each)
-            _, _, info = tab.bkt_probe(key[reach], 0, int(os.environ.get("COP_BKT_XBITS", "1")))
+            _, _, info = tab.bkt_probe(key[reach], 1 if name == "fw" else 0, int(os.environ.get("COP_BKT_XBITS", "1")))
             out[name] = {"form": "bkt (bucketed intervals, L2)", "ib": info["ib"],
                          "l2_loads_per_pkt": round((2 * float(reach.sum()) + 2 * info["rounds"]) / n, 4),
                          "wide_lookups_per_pkt": round(info["lifted"] / n, 4),
@@ -283,6 +283,7 @@ def measure(args, name, rank, world, dev, group, gate, primary):
     ctx = cg.Context(device=dev, stages=stages, max_batch=B, max_batches=32, n_streams=args.streams,
                      flags=(cg.CFG_RULE_COUNTERS if rc_on else 0) | (cg.CFG_NO_COMPACT if args.no_compact else 0)
                      | {"dir": 0, "trie": cg.CFG_LPM_TRIE, "bkt": cg.CFG_LPM_BKT}[args.route_form]
+                     | (cg.CFG_FW_BKT if args.fw_form == "bkt" else 0)
                      | (cg.CFG_SEG_LISTS if seg else 0))
     ctx.set_fw_table(fw_tab)
     coll = None
@@ -317,11 +318,13 @@ def measure(args, name, rank, world, dev, group, gate, primary):
         pool_bytes = max(400 << 20, per_batch * Lb)
     P = max(2, pool_bytes // per_batch)
     d_pkts = ctx.alloc(P * per_batch)
-    d_res = ctx.alloc(P * B * 8)
-    d_fwd = ctx.alloc(P * B * 4)
+    # outputs: HBM, or (A/B) uncached / fine-grained HBM (--out-mem)
+    of = {"device": 0, "uncached": cg.ALLOC_UNCACHED, "fine": cg.ALLOC_FINEGRAINED}[args.out_mem]
+    d_res = ctx.alloc(P * B * 8, of)
+    d_fwd = ctx.alloc(P * B * 4, of)
     n_seg = (B + cg.SEG_PKTS - 1) // cg.SEG_PKTS
     cnt_per_slot = n_seg if seg else 1   # one count per segment, or per batch
-    d_cnt = ctx.alloc(P * cnt_per_slot * 4 + 16)
+    d_cnt = ctx.alloc(P * cnt_per_slot * 4 + 16, of)
     if W["imix"]:
         # same packet mix in every batch slot, distinct addresses
         for i in range(P):
@@ -516,10 +519,10 @@ def measure(args, name, rank, world, dev, group, gate, primary):
     res.update(bytes_per_pkt=bytes_per_pkt, alg_bytes=alg_bytes, achieved=achieved, total_pkts=total_pkts)
     try:   # a report only: never fails the line
         if W["imix"]:
-            probes = table_probes(fw_tab, rt_tab, slab, offs, args.route_form)
+            probes = table_probes(fw_tab, rt_tab, slab, offs, args.route_form, args.fw_form)
         else:
             sample = cg.gen_trace(copdist.shard_seed(0x5EED0000 + cid, rank, 0), B, fw_rules, routes)
-            probes = table_probes(fw_tab, rt_tab, sample, None, args.route_form)
+            probes = table_probes(fw_tab, rt_tab, sample, None, args.route_form, args.fw_form)
     except Exception as e:  # noqa: BLE001
         probes = {"error": repr(e)}
     res["probes"] = probes
@@ -648,6 +651,12 @@ def main():
                     help="poll-mode slot declaration: static = the pool is written once before the start "
                          "(COP_PMD_STATIC_SLOTS, no acquire); reuse = the default of cop_pmd_start (a system-scope "
                          "acquire per tile once the ring wraps); always = an acquire on every tile")
+    ap.add_argument("--fw-form", default="dir", choices=("dir", "bkt"),
+                    help="firewall tables too large for LDS (1M rules): DIR-24-8 image, or the bucketed intervals "
+                         "keyed by rule id (COP_CFG_FW_BKT)")
+    ap.add_argument("--out-mem", default="device", choices=("device", "uncached", "fine"),
+                    help="A/B: the ring's records, lists and counts in HBM (default), uncached HBM or fine-grained "
+                         "HBM (cop_dev_alloc_ex)")
     ap.add_argument("--deadline", type=float, default=1500.0,
                     help="seconds after which a rank that has not finished exits with status 124 (a hung rank "
                          "must not hold the driver's node)")
@@ -799,6 +808,7 @@ def main():
             "fw_rules": W["fw"],
             "route_prefixes": W["routes"],
             "route_form": args.route_form if W["routes"] else None,
+            "fw_form": args.fw_form if W["fw"] > 8192 else "lds-intervals",
             "slots": args.slots if res["engine"] == "pmd" else None,
             "pkt_layout": "imix slab + u32 offsets" if W["imix"] else "64B slots",
             "stages": args.stages or W["stages"],
@@ -865,7 +875,8 @@ def main():
                 "value_union": round(sres["windows"]["value_union"], 3),
                 "batch": sres["B"], "fw_rules": sres["W"]["fw"], "route_prefixes": sres["W"]["routes"],
                 "pkt_layout": "imix slab + u32 offsets" if sres["W"]["imix"] else "64B slots",
-                "route_form": args.route_form, "rule_counters": sres["rc_on"], "roofline": sroof}
+                "route_form": args.route_form, "fw_form": args.fw_form if sres["W"]["fw"] > 8192 else "lds-intervals",
+                "rule_counters": sres["rc_on"], "roofline": sroof}
             if sres["rc_on"]:
                 blk["rccl_init"] = group.gather_obj(sres["coll"])
             if "reduce_info" in sres:

@@ -26,6 +26,7 @@ LPM_STOP_AT_FIRST_ERROR = 0x1
 CFG_FW_FORCE_DIR24, CFG_LPM_FORCE_DIR24, CFG_NO_COMPACT, CFG_RULE_COUNTERS = 0x1, 0x2, 0x4, 0x8
 CFG_DEMUX_PORTS, CFG_PORT_STATS, CFG_LPM_TRIE, CFG_SEG_LISTS = 0x10, 0x20, 0x40, 0x80
 CFG_LPM_BKT = 0x100
+CFG_FW_BKT = 0x200
 SEG_PKTS = 256   # COP_SEG_PKTS: packets per forward-list segment (CFG_SEG_LISTS)
 MAX_DEMUX_PORTS = 8
 GEN_FW, GEN_ROUTES = 0, 1
@@ -157,6 +158,7 @@ SIGNATURES = {
     "cop_coll_init": (c_int, [c_void_p, c_void_p, c_int, c_int]),
     "cop_coll_reduce_counters": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_int]),
     "cop_dev_alloc": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
+    "cop_dev_alloc_ex": (c_int, [c_void_p, c_size_t, c_uint32, POINTER(c_void_p)]),
     "cop_dev_free": (c_int, [c_void_p, c_void_p]),
     "cop_host_alloc_pinned": (c_int, [c_void_p, c_size_t, POINTER(c_void_p)]),
     "cop_host_alloc_mapped": (c_int, [c_void_p, c_size_t, POINTER(c_void_p), POINTER(c_void_p)]),
@@ -416,12 +418,18 @@ class LpmTable:
         return t24, t8[: n_ext * 256]
 
 
+ALLOC_UNCACHED, ALLOC_FINEGRAINED = 1, 2
+
+
 class DeviceBuffer:
-    def __init__(self, ctx: "Context", nbytes: int):
+    def __init__(self, ctx: "Context", nbytes: int, flags: int = 0):
         self.ctx = ctx
         self.nbytes = int(nbytes)
         self.ptr = c_void_p()
-        _check(lib().cop_dev_alloc(ctx.handle, self.nbytes, byref(self.ptr)), ctx, "dev_alloc")
+        if flags:
+            _check(lib().cop_dev_alloc_ex(ctx.handle, self.nbytes, flags, byref(self.ptr)), ctx, "dev_alloc_ex")
+        else:
+            _check(lib().cop_dev_alloc(ctx.handle, self.nbytes, byref(self.ptr)), ctx, "dev_alloc")
 
     @property
     def addr(self) -> int:
@@ -545,8 +553,9 @@ class Context:
                "load_fw_rules_file")
         return rep
 
-    def alloc(self, nbytes) -> DeviceBuffer:
-        return DeviceBuffer(self, nbytes)
+    def alloc(self, nbytes, flags: int = 0) -> DeviceBuffer:
+        """HBM (flags: ALLOC_UNCACHED / ALLOC_FINEGRAINED, cop_dev_alloc_ex)."""
+        return DeviceBuffer(self, nbytes, flags)
 
     def pmd_start(self, ring, flags: int = 0) -> "Pmd":
         """Start the poll-mode (persistent) kernel serving `ring` (or a list

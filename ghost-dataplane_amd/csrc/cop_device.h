@@ -386,10 +386,39 @@ __device__ __forceinline__ StepGeom step_geom(int lane)
     return g;
 }
 
-// the three loads of the step starting at packet pb (clamped to `last`)
-__device__ __forceinline__ void load_step(const StepGeom &g, const uint8_t *pk0, uint32_t stride, uint32_t pb,
-                                          uint32_t last, u32x4 (&v)[3])
+// System-coherent loads (sc0 sc1) at byte offset off of base: no L1 or L2
+// copy is used, so a ring slot another agent rewrote since this launch last
+// read it is read afresh (offsets below 2^31: one batch of a ring slot)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(const void *base)
 {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ u32x4 ld_sys16(__amdgpu_buffer_rsrc_t rs, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 1 | 16);
+}
+__device__ __forceinline__ u32x2 ld_sys8(__amdgpu_buffer_rsrc_t rs, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 1 | 16);
+}
+__device__ __forceinline__ uint32_t ld_sys4(__amdgpu_buffer_rsrc_t rs, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 1 | 16);
+}
+
+// the three loads of the step starting at packet pb (clamped to `last`).
+// sys: system-coherent loads (sc0 sc1: no L1 or L2 copy of the slot is
+// used), for ring slots another agent may have rewritten since this launch
+// last read them, instead of an acquire that invalidates the caches
+__device__ __forceinline__ void load_step(const StepGeom &g, const uint8_t *pk0, uint32_t stride, uint32_t pb,
+                                          uint32_t last, u32x4 (&v)[3], bool sys = false)
+{
+    if (sys) {
+        const __amdgpu_buffer_rsrc_t rs = sys_rsrc(pk0);
+#pragma unroll
+        for (int c = 0; c < 3; c++) v[c] = ld_sys16(rs, min(pb + g.lpk[c], last) * stride + g.lch[c]);
+        return;
+    }
 #pragma unroll
     for (int c = 0; c < 3; c++) {
         const uint32_t ic = min(pb + g.lpk[c], last);
@@ -465,7 +494,7 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
                                       const uint32_t (&w6)[PPT], const uint32_t (&w7)[PPT],
                                       const uint32_t (&w8)[PPT], uint32_t (&verdict)[PPT], uint32_t (&port)[PPT],
                                       uint32_t (&src)[PPT], uint32_t (&dst)[PPT], uint32_t (&fwe)[PPT],
-                                      uint32_t (&lpe)[PPT], uint32_t (&lpe2)[PPT])
+                                      uint32_t (&lpe)[PPT], uint32_t (&lpe2)[PPT], uint32_t (&fwe2)[PPT])
 {
     const bool stageP = (p.stages & COPK_STAGE_PARSE) != 0;
 #pragma unroll
@@ -493,6 +522,7 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
         const bool reach = verdict[k] == COPK_FORWARD;
         if (FW == COPK_TBL_IVT) fwe[k] = t.fw_v[ivt_search(t.fw_s, p.fw_m, p.fw_ib, p.fw_lv, src[k])];
         if (FW == COPK_TBL_DIR) fwe[k] = reach ? probe_ld(&p.fw_tbl24[src[k] >> 8], p.probe_nt) : 0u;
+        if (FW == COPK_TBL_BKT) bkt_issue(p.fw_bidx, p.fw_ib, src[k], reach, fwe[k], fwe2[k]);
         if (LPM == COPK_TBL_IVT) lpe[k] = t.lp_v[ivt_search(t.lp_s, p.lpm_m, p.lpm_ib, p.lpm_lv, dst[k])];
         if (LPM == COPK_TBL_DIR) lpe[k] = reach ? probe_ld(&p.lpm_tbl24[dst[k] >> 8], p.probe_nt) : 0u;
         if (LPM == COPK_TBL_TRIE) lpe[k] = t.lp_s[dst[k] >> 20];
@@ -659,9 +689,9 @@ __device__ __forceinline__ void bkt_step(const uint32_t *pairs, const uint32_t (
 template <int FW, int LPM, int PPT>
 __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[PPT], const uint32_t (&src)[PPT],
                                       const uint32_t (&dst)[PPT], const bool (&valid)[PPT], uint32_t (&fwe)[PPT],
-                                      uint32_t (&lpe)[PPT], const uint32_t (&lpe2)[PPT], uint32_t (&verdict)[PPT],
-                                      uint32_t (&flags)[PPT], uint32_t (&rnh)[PPT], uint32_t &c_total,
-                                      uint32_t &c_notv4)
+                                      uint32_t (&lpe)[PPT], const uint32_t (&lpe2)[PPT], const uint32_t (&fwe2)[PPT],
+                                      uint32_t (&verdict)[PPT], uint32_t (&flags)[PPT], uint32_t (&rnh)[PPT],
+                                      uint32_t &c_total, uint32_t &c_notv4)
 {
     bool reached[PPT];
 #pragma unroll
@@ -671,6 +701,7 @@ __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[
         rnh[k] = 0;
     }
     if (FW == COPK_TBL_DIR) tbl8_step<PPT>(p.fw_tbl8, p.fw_tbl8_packed, src, fwe);
+    if (FW == COPK_TBL_BKT) bkt_step<PPT>(p.fw_bpairs, src, fwe, fwe2, reached);
     if (LPM == COPK_TBL_DIR) tbl8_step<PPT>(p.lpm_tbl8, p.lpm_tbl8_packed, dst, lpe);
     if (LPM == COPK_TBL_TRIE) trie_walk<PPT>(p.lpm_tnodes, p.lpm_tleaves, dst, lpe, reached);
     if (LPM == COPK_TBL_BKT) bkt_step<PPT>(p.lpm_bpairs, dst, lpe, lpe2, reached);

@@ -23,7 +23,7 @@ static_assert(sizeof(void *) == 8, "64-bit only");
 #define COPK_TBL_DIR 2  /* DIR-24-8 image in HBM */
 #define COPK_TBL_TRIE 3 /* multibit trie: 12-bit top level in LDS, 6-bit popcount nodes in L2 (route stage) */
 #define COPK_TBL_BKT 4  /* bucketed intervals in global memory (L2): first candidate per top-ib-bit bucket,
-                           then (start, value) pairs (route stage) */
+                           then (start, value) pairs (route stage; firewall stage with COP_CFG_FW_BKT) */
 #define COPK_TRIE_L0 4096u
 /* Packed tbl8 form of a DIR-24-8 image: an extended tbl24 entry's payload is
  * the offset (in 64-byte units) of its /24's run block instead of a group
@@ -115,6 +115,9 @@ struct CopKParams {
     // {0xFFFFFFFF, last value} pairs); lpm_lv lifting levels above the
     // widest bucket
     const uint32_t *lpm_bidx, *lpm_bpairs;
+    // the firewall table in the same bucketed form (COPK_TBL_BKT firewall,
+    // COP_CFG_FW_BKT: 1M-rule tables; fw_ib its index bits)
+    const uint32_t *fw_bidx, *fw_bpairs;
     // LDS carve (u32 words)
     uint32_t lds_fw_off, lds_lpm_off, lds_misc_off;
     uint32_t lds_stage_off;   // one-shot kernel: the tile's forward list staged in LDS (0: none)
@@ -190,8 +193,10 @@ struct CopKPmd {
     uint32_t n_work;                     // worker workgroups
     uint32_t relay_stride;               // every relay_stride-th worker also reads the host doorbell
     uint32_t stepwise;                   // tiles step by step where tile_steps applies ($COP_PMD_STEPWISE=0: off)
-    uint32_t sys_acquire;                // system-scope acquire before a tile's loads: 0 never (static slots),
-                                         // 1 every tile (host-memory rings), 2 once the ring wraps in this launch
+    uint32_t sys_acquire;                // slot reuse: 0 plain loads (static slots); system-coherent packet
+                                         // loads on every tile (3: host-memory rings) or once the ring wraps in
+                                         // this launch (4: the default); A/B only: a system-scope acquire before
+                                         // the loads instead, every tile (1) / once wrapped (2)
     uint32_t test_skip;                  // tests: tile test_skip - 1 of ring 0's batch 0 never runs ($COP_PMD_TEST_SKIP_TILE)
     uint32_t poll_backoff;               // waiting workers' s_sleep(4) rounds between relay polls once idle
                                          // (3: ~0.3 us, the default; 0: busy polling, $COP_PMD_BACKOFF)
@@ -201,8 +206,11 @@ struct CopKPmd {
     // claims its next tile and issues that tile's header loads before it
     // finishes the current one ($COP_PMD_DYN)
     uint32_t dyn;
-    unsigned long long *d_ticket;        // device: ring r's claim counter at [16 r] (zeroed at every launch)
+    uint32_t tk_lanes;                   // ticket lanes per ring (1, or 8: one per XCD-sized worker group)
+    unsigned long long *d_ticket;        // device: ring r's lane x claim counter at [16 (r * COPK_PMD_TK_LANES + x)]
+                                         // (zeroed at every launch)
 };
+#define COPK_PMD_TK_LANES 8
 #define COPK_PMD_RELAYS 8
 #define COPK_PMD_GATE_SHIFT 56
 #define COPK_PMD_RUNNING 0u

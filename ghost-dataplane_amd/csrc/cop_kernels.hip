@@ -154,6 +154,14 @@ template <int FW>
 hipError_t launch_lpm(const CopKParams &p, int lpm, int imix, int ppt, uint32_t grid, uint32_t lds,
                       hipStream_t s)
 {
+    if constexpr (FW == COPK_TBL_BKT) {
+        // the bucketed firewall (1M-rule tables) beside the large route forms
+        // only: a route table small enough for LDS goes with a small firewall
+        if (lpm == COPK_TBL_DIR) return launch_imix<FW, COPK_TBL_DIR>(p, imix, ppt, grid, lds, s);
+        if (lpm == COPK_TBL_BKT) return launch_imix<FW, COPK_TBL_BKT>(p, imix, ppt, grid, lds, s);
+        if (lpm == COPK_TBL_OFF) return launch_imix<FW, COPK_TBL_OFF>(p, imix, ppt, grid, lds, s);
+        return hipErrorInvalidValue;
+    }
     if (lpm == COPK_TBL_IVT) return launch_imix<FW, COPK_TBL_IVT>(p, imix, ppt, grid, lds, s);
     if (lpm == COPK_TBL_DIR) return launch_imix<FW, COPK_TBL_DIR>(p, imix, ppt, grid, lds, s);
     if (lpm == COPK_TBL_TRIE) return launch_imix<FW, COPK_TBL_TRIE>(p, imix, ppt, grid, lds, s);
@@ -172,6 +180,7 @@ hipError_t launch_lpm(const CopKParams &p, int lpm, int imix, int ppt, uint32_t 
 extern "C" hipError_t copk_launch_fw0(COPK_LAUNCH_ARGS);
 extern "C" hipError_t copk_launch_fw1(COPK_LAUNCH_ARGS);
 extern "C" hipError_t copk_launch_fw2(COPK_LAUNCH_ARGS);
+extern "C" hipError_t copk_launch_fw4(COPK_LAUNCH_ARGS);
 #if defined(COPK_FW_PART)
 #define COPK_CAT2(a, b) a##b
 #define COPK_CAT(a, b) COPK_CAT2(a, b)
@@ -180,12 +189,13 @@ extern "C" hipError_t COPK_CAT(copk_launch_fw, COPK_FW_PART)(COPK_LAUNCH_ARGS)
     return launch_lpm<COPK_FW_PART>(*p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
 }
 #else
-static_assert(COPK_TBL_OFF == 0 && COPK_TBL_IVT == 1 && COPK_TBL_DIR == 2, "part numbering");
+static_assert(COPK_TBL_OFF == 0 && COPK_TBL_IVT == 1 && COPK_TBL_DIR == 2 && COPK_TBL_BKT == 4, "part numbering");
 extern "C" hipError_t copk_launch(const CopKParams *p, int fw_mode, int lpm_mode, int imix, int ppt,
                                   uint32_t grid, uint32_t lds_bytes, hipStream_t stream)
 {
     if (fw_mode == COPK_TBL_IVT) return copk_launch_fw1(p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
     if (fw_mode == COPK_TBL_DIR) return copk_launch_fw2(p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
+    if (fw_mode == COPK_TBL_BKT) return copk_launch_fw4(p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
     return copk_launch_fw0(p, lpm_mode, imix, ppt, grid, lds_bytes, stream);
 }
 

@@ -327,14 +327,20 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             // Slot reuse: another agent (the host, a copy engine, a NIC) may
             // have rewritten the slot since this CU (or its XCD's L2) last
             // read it, and a persistent kernel gets no dispatch-time cache
-            // invalidation, so the tile acquires at system scope before its
-            // loads (the doorbell read that made the batch visible came
-            // first). Mode 2 (the default): only from the ring's second lap
-            // in this launch on; a slot's first read in a launch follows the
-            // launch's own invalidation. Mode 1: every tile (host-memory
-            // rings, COP_PMD_SYS_ACQUIRE). Mode 0: never (COP_PMD_STATIC_SLOTS).
-            if (P.sys_acquire == 1u || (P.sys_acquire == 2u && b >= P.seq0r[r] + n_slots))
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            // invalidation. So the tile reads the slot with system-coherent
+            // loads (sc0 sc1: no cached copy is used; the doorbell read that
+            // made the batch visible came first): mode 4, the default, from
+            // the ring's second lap in this launch on (a slot's first read in
+            // a launch follows the launch's own invalidation); mode 3 on every
+            // tile (host-memory rings, COP_PMD_SYS_ACQUIRE); mode 0 never
+            // (COP_PMD_STATIC_SLOTS). Modes 1 / 2 (A/B runs, $COP_PMD_ACQUIRE)
+            // acquire at system scope instead, every tile / once wrapped: an
+            // acquire invalidates the CU's and the XCD's caches for every
+            // worker there, which halved the driver's 20-step rate
+            // (profiles/r05/check2/acq*.log).
+            const bool wrapped = b >= P.seq0r[r] + n_slots;
+            const bool sysld = P.sys_acquire == 3u || (P.sys_acquire == 4u && wrapped);
+            if (P.sys_acquire == 1u || (P.sys_acquire == 2u && wrapped)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             // The lane's index is made opaque each iteration, so the per-lane
             // values the tile derives from it (load geometry, LDS addresses) are
             // recomputed in the tile rather than hoisted out of the loop and held
@@ -348,7 +354,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             if constexpr (STEPS) {
                 if (j < ntiles)   // (a tile past a short batch's packets has nothing to do)
                     tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, pmd_batch(p, rg, slot, n, ntiles), j, tid_i,
-                                                                lane_i, wave_i);
+                                                                lane_i, wave_i, sysld);
             } else {
                 if (P.test_skip && r == 0 && b == 0 && j + 1 == P.test_skip) {
                     ok = false;   // tests: this tile never runs nor publishes (its successors give up)
@@ -364,7 +370,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                     const LookCtx lk{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0], P.test_skip ? 14u : 22u};
                     ok = tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
                         p, o, lc, pmd_batch(p, rg, slot, n, ntiles), (rs0 + slot) * tpb, j, lk, tid_i, lane_i, wave_i,
-                        false, (size_t)(rs0 + slot) * tpb + j);
+                        false, (size_t)(rs0 + slot) * tpb + j, sysld);
                 }
             }
             if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done
@@ -404,7 +410,16 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         constexpr bool STEPS = decltype(steps_c)::value && PPT <= 2;
         if constexpr (STEPS) {
             constexpr int W = COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT;
-            unsigned long long *ticket = P.d_ticket + (size_t)r * 16;
+            // ticket lanes: one per XCD-sized group of the ring's workers
+            // (worker wr claims from lane wr % nx; with one ring that is its
+            // XCD, workgroups being dealt round-robin over the 8 XCDs), lane
+            // x owning tiles j = x, x + nx, ... of every batch, so no one
+            // counter takes every claim (one counter for all 1536 workers
+            // held a 256-packet-tile kernel at ~80 claims per us)
+            const uint32_t nx = (P.tk_lanes > 1 && tpb % P.tk_lanes == 0) ? P.tk_lanes : 1u;
+            const uint32_t xl = wr % nx;
+            const uint32_t per = tpb / nx;   // tiles of one batch in one lane
+            unsigned long long *ticket = P.d_ticket + ((size_t)r * COPK_PMD_TK_LANES + xl) * 16;
             uint32_t *s_tk = lc.s_misc + 72;   // the next claimed ticket (lo, hi)
             unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
             const bool leader = wr % P.relay_stride == 0;
@@ -450,8 +465,8 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                 asm volatile("" : "+v"(tid_i));
                 const int lane_i = tid_i & 63;
                 const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
-                const unsigned long long b = seq0 + T / tpb;
-                const uint32_t j = (uint32_t)(T % tpb);
+                const unsigned long long b = seq0 + T / per;
+                const uint32_t j = (uint32_t)(T % per) * nx + xl;
                 const uint32_t slot = (uint32_t)(b % n_slots);
                 if (stamp && tid == 0) {
                     st_stamp(&stamp[0], __builtin_amdgcn_s_memrealtime());   // diagnostic: tile start
@@ -483,21 +498,27 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                         lds_barrier();
                     }
                     ntiles = (n + TILE - 1) / TILE;
-                    if (P.sys_acquire == 1u || (P.sys_acquire == 2u && b >= seq0 + n_slots))
+                    const bool wrapped = b >= seq0 + n_slots;
+                    if (P.sys_acquire == 1u || (P.sys_acquire == 2u && wrapped))
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                    if (j < ntiles) steps_load<PPT, 0, W>(pmd_batch(p, rg, slot, n, ntiles), j, lane_i, wave_i, cur);
+                    const bool sysld = P.sys_acquire == 3u || (P.sys_acquire == 4u && wrapped);
+                    if (j < ntiles)
+                        steps_load<PPT, 0, W>(pmd_batch(p, rg, slot, n, ntiles), j, lane_i, wave_i, cur, sysld);
                 }
                 if (stamp && tid == 0) st_stamp(&stamp[1], __builtin_amdgcn_s_memrealtime());   // loads issued
                 // the next tile's loads, before this tile's work, when its
                 // batch is known posted (fixed-size batches)
-                const unsigned long long bn = seq0 + Tn / tpb;
-                const uint32_t jn = (uint32_t)(Tn % tpb);
+                const unsigned long long bn = seq0 + Tn / per;
+                const uint32_t jn = (uint32_t)(Tn % per) * nx + xl;
                 const uint32_t sn = (uint32_t)(bn % n_slots);
                 const bool pf = bn < posted && !P.h_n;
                 if (pf) {
-                    if (P.sys_acquire == 1u || (P.sys_acquire == 2u && bn >= seq0 + n_slots))
+                    const bool wrapped = bn >= seq0 + n_slots;
+                    if (P.sys_acquire == 1u || (P.sys_acquire == 2u && wrapped))
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                    if (jn < ntiles) steps_load<PPT, 0, W>(pmd_batch(p, rg, sn, rg.n, ntiles), jn, lane_i, wave_i, nxt);
+                    const bool sysld = P.sys_acquire == 3u || (P.sys_acquire == 4u && wrapped);
+                    if (jn < ntiles)
+                        steps_load<PPT, 0, W>(pmd_batch(p, rg, sn, rg.n, ntiles), jn, lane_i, wave_i, nxt, sysld);
                 }
                 // and the claim after it
                 unsigned long long tnn = 0;
@@ -583,6 +604,12 @@ hipError_t pmd_lpm(const CopKPmd *p, int lpm, int lay, int ppt, int ext, uint32_
 #ifdef COPK_ISA_PROBE   // ISA inspection builds only: one instantiation (tools/isa.sh)
     return pmd_one<FW, COPK_TBL_OFF, COPK_LAY_COALESCED, COPK_ISA_PROBE>(p, ext, lds, s, occ);
 #else
+    if constexpr (FW == COPK_TBL_BKT) {   // as cop_kernels.hip launch_lpm
+        if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);
+        if (lpm == COPK_TBL_BKT) return pmd_lay<FW, COPK_TBL_BKT>(p, lay, ppt, ext, lds, s, occ);
+        if (lpm == COPK_TBL_OFF) return pmd_lay<FW, COPK_TBL_OFF>(p, lay, ppt, ext, lds, s, occ);
+        return hipErrorInvalidValue;
+    }
     if (lpm == COPK_TBL_IVT) return pmd_lay<FW, COPK_TBL_IVT>(p, lay, ppt, ext, lds, s, occ);
     if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);
     if (lpm == COPK_TBL_TRIE) return pmd_lay<FW, COPK_TBL_TRIE>(p, lay, ppt, ext, lds, s, occ);
@@ -598,6 +625,7 @@ hipError_t pmd_lpm(const CopKPmd *p, int lpm, int lay, int ppt, int ext, uint32_
 extern "C" hipError_t copk_pmd_fw0(COPK_PMD_ARGS);
 extern "C" hipError_t copk_pmd_fw1(COPK_PMD_ARGS);
 extern "C" hipError_t copk_pmd_fw2(COPK_PMD_ARGS);
+extern "C" hipError_t copk_pmd_fw4(COPK_PMD_ARGS);
 #if defined(COPK_FW_PART)
 #define COPK_CAT2(a, b) a##b
 #define COPK_CAT(a, b) COPK_CAT2(a, b)
@@ -611,6 +639,7 @@ static hipError_t pmd_dispatch(const CopKPmd *p, int fw, int lpm, int lay, int p
 {
     if (fw == COPK_TBL_IVT) return copk_pmd_fw1(p, lpm, lay, ppt, ext, lds, s, occ);
     if (fw == COPK_TBL_DIR) return copk_pmd_fw2(p, lpm, lay, ppt, ext, lds, s, occ);
+    if (fw == COPK_TBL_BKT) return copk_pmd_fw4(p, lpm, lay, ppt, ext, lds, s, occ);
     return copk_pmd_fw0(p, lpm, lay, ppt, ext, lds, s, occ);
 }
 

@@ -534,6 +534,11 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
         else if (!strcmp(e, "bkt")) c->cfg.flags = (c->cfg.flags & ~COP_CFG_LPM_TRIE) | COP_CFG_LPM_BKT;
         else if (!strcmp(e, "dir")) c->cfg.flags &= ~(COP_CFG_LPM_TRIE | COP_CFG_LPM_BKT);
     }
+    // firewall-table form for tables too large for LDS (A/B runs): bkt | dir
+    if (const char *e = getenv("COP_FW_FORM")) {
+        if (!strcmp(e, "bkt")) c->cfg.flags |= COP_CFG_FW_BKT;
+        else if (!strcmp(e, "dir")) c->cfg.flags &= ~COP_CFG_FW_BKT;
+    }
     if (const char *e = getenv("COP_STREAMS")) {
         int v = atoi(e);
         if (v >= 1 && v <= MAX_LANES) cfg.n_streams = (uint32_t)v;
@@ -792,7 +797,8 @@ int cop_set_fw_table(cop_ctx *c, const cop_lpm_table *t)
     if (!c || !t) return -EINVAL;
     if (c->pmd) return set_err(c, -EBUSY, "a poll-mode kernel is serving this context (cop_pmd_stop first)");
     if (t->n_rules > COP_LPM_NH_MASK) return set_err(c, -EINVAL, "rule ids exceed 24 bits");
-    int rc = upload_lpm(c, c->fw, t, !(c->cfg.flags & COP_CFG_FW_FORCE_DIR24), COP_FORM_RULE);
+    int rc = upload_lpm(c, c->fw, t, !(c->cfg.flags & COP_CFG_FW_FORCE_DIR24), COP_FORM_RULE, false,
+                        (c->cfg.flags & COP_CFG_FW_BKT) != 0);
     if (rc) {
         // a failed upload leaves the stage with the empty table (every lookup
         // misses), never with a partial image a launch could read
@@ -966,6 +972,8 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
     p.lpm_tleaves = c->lpm.tleaves;
     p.lpm_bidx = c->lpm.bidx;
     p.lpm_bpairs = c->lpm.bpairs;
+    p.fw_bidx = c->fw.bidx;
+    p.fw_bpairs = c->fw.bpairs;
     uint32_t off = 256 + c->rt_nleaf * 128;
     p.lds_fw_off = off;
     off += 2 * p.fw_m + p.fw_iw;
@@ -1883,6 +1891,16 @@ int cop_dev_alloc(cop_ctx *c, size_t bytes, void **dptr)
     return 0;
 }
 
+int cop_dev_alloc_ex(cop_ctx *c, size_t bytes, uint32_t flags, void **dptr)
+{
+    if (!c || !dptr || (flags != 0 && flags != COP_ALLOC_UNCACHED && flags != COP_ALLOC_FINEGRAINED)) return -EINVAL;
+    if (!flags) return cop_dev_alloc(c, bytes, dptr);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipExtMallocWithFlags(dptr, bytes ? bytes : 16,
+                                    flags == COP_ALLOC_UNCACHED ? hipDeviceMallocUncached : hipDeviceMallocFinegrained));
+    return 0;
+}
+
 int cop_dev_free(cop_ctx *c, void *dptr)
 {
     if (!c) return -EINVAL;
@@ -2011,7 +2029,7 @@ struct cop_pmd {
     uint8_t *dev = nullptr;                 // device words: ctl, gates, relays, slot tile counts, look-back
     size_t dev_bytes = 0;
     uint32_t n_rings = 1, n_slots = 0, tpb = 0, per_cu = 0, ring_n = 0;
-    uint32_t acquire = 2;       // CopKPmd::sys_acquire: 2 on slot reuse (default), 1 every tile, 0 never
+    uint32_t acquire = 4;       // CopKPmd::sys_acquire: 4 coherent loads on slot reuse (default), 3 on every tile, 0 never
     bool dyn = false;           // CopKPmd::dyn: dynamic tiles
     std::atomic<uint32_t> launches{0};
     uint32_t pauses = 0;                    // pmd_pause calls that stopped a running kernel
@@ -2041,7 +2059,7 @@ constexpr size_t PMD_ACT_OFF = 64;
 constexpr size_t PMD_GATE_OFF = 1024;
 constexpr size_t PMD_RELAY_OFF = 2048;
 constexpr size_t PMD_TICKET_OFF = PMD_RELAY_OFF + 128 * COPK_PMD_RELAYS * COPK_PMD_MAX_RINGS;   // dynamic tiles
-constexpr size_t PMD_CTL_BYTES = PMD_TICKET_OFF + 128 * COPK_PMD_MAX_RINGS;
+constexpr size_t PMD_CTL_BYTES = PMD_TICKET_OFF + 128 * COPK_PMD_TK_LANES * COPK_PMD_MAX_RINGS;
 static_assert(PMD_GATE_OFF + 128 * COPK_PMD_MAX_RINGS <= PMD_RELAY_OFF, "gates overlap relays");
 static_assert(64 * COPK_PMD_MAX_RINGS <= PMD_H_STOP, "posted words overlap the stop word");
 
@@ -2179,26 +2197,29 @@ static void pmd_size(cop_pmd *m)
     m->P.poll_backoff = 3;
     m->P.stepwise = getenv("COP_PMD_STEPWISE") && !atoi(getenv("COP_PMD_STEPWISE")) ? 0u : 1u;
     m->P.dyn = m->dyn ? 1u : 0u;
+    // ticket lanes of dynamic tiles: 8 unless $COP_PMD_TK_LANES says 1
+    m->P.tk_lanes = COPK_PMD_TK_LANES;
+    if (const char *e = getenv("COP_PMD_TK_LANES")) m->P.tk_lanes = atoi(e) == 1 ? 1u : (uint32_t)COPK_PMD_TK_LANES;
     if (const char *e = getenv("COP_PMD_BACKOFF")) m->P.poll_backoff = std::min(64u, (uint32_t)atoi(e));
     // Slot reuse (switch.c:463-470: the fast path refills the rings
     // forever): a ring slot may be rewritten by another agent between its
     // batches, and a persistent kernel gets no dispatch-time invalidation, so
-    // by default a tile acquires at system scope before its loads once its
-    // ring has wrapped in this launch (mode 2; a slot's first read in a
+    // by default a tile reads its slot with system-coherent loads once its
+    // ring has wrapped in this launch (mode 4; a slot's first read in a
     // launch is fresh). Rings whose packets live in host memory (mapped
-    // pinned: the drop-in's header records) acquire on every tile (mode 1,
+    // pinned: the drop-in's header records) do so on every tile (mode 3,
     // also COP_PMD_SYS_ACQUIRE); COP_PMD_STATIC_SLOTS declares the slots
-    // written once before the start (mode 0: no acquire).
+    // written once before the start (mode 0: plain loads).
     m->P.sys_acquire = m->acquire;
-    if (m->acquire == 2u) {
+    if (m->acquire == 4u) {
         for (uint32_t q = 0; q < m->n_rings; q++) {
             hipPointerAttribute_t at;
             if (hipPointerGetAttributes(&at, m->P.rings[q].pkts) == hipSuccess && at.type == hipMemoryTypeHost)
-                m->P.sys_acquire = 1;
+                m->P.sys_acquire = 3;
         }
         (void)hipGetLastError();   // (an unregistered pointer leaves an error behind)
     }
-    if (const char *e = getenv("COP_PMD_ACQUIRE")) m->P.sys_acquire = std::min(2u, (uint32_t)atoi(e));   // A/B runs
+    if (const char *e = getenv("COP_PMD_ACQUIRE")) m->P.sys_acquire = std::min(4u, (uint32_t)atoi(e));   // A/B runs
     // tests: a tile that never runs, so its successors' look-back gives up
     m->P.test_skip = getenv("COP_PMD_TEST_SKIP_TILE") ? (uint32_t)atoi(getenv("COP_PMD_TEST_SKIP_TILE")) + 1u : 0u;
 }
@@ -2377,7 +2398,7 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
     m->c = c;
     m->n_rings = n_rings;
     m->ring_n = r->n;
-    m->acquire = (flags & COP_PMD_SYS_ACQUIRE) ? 1u : (flags & COP_PMD_STATIC_SLOTS) ? 0u : 2u;
+    m->acquire = (flags & COP_PMD_SYS_ACQUIRE) ? 3u : (flags & COP_PMD_STATIC_SLOTS) ? 0u : 4u;
     Plan pl = plan_launch(c, (uint64_t)r->n * r->n_slots, imix, r->stride);
     // tile size: 1024-packet tiles (five workers per CU, so a 20-batch burst
     // of 64k packets is one tile per worker), 256-packet tiles for small

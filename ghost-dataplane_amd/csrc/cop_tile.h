@@ -188,8 +188,8 @@ __device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &
 template <int FW, int LPM, int LAY, bool EXT>
 constexpr bool steps_ok()
 {
-    return !EXT && LAY == COPK_LAY_COALESCED && FW != COPK_TBL_DIR && LPM != COPK_TBL_DIR && LPM != COPK_TBL_TRIE &&
-           LPM != COPK_TBL_BKT;
+    return !EXT && LAY == COPK_LAY_COALESCED && FW != COPK_TBL_DIR && FW != COPK_TBL_BKT && LPM != COPK_TBL_DIR &&
+           LPM != COPK_TBL_TRIE && LPM != COPK_TBL_BKT;
 }
 
 // One tile of the poll-mode kernel, step by step (tile_body does the same
@@ -217,14 +217,15 @@ constexpr bool steps_ok()
 // window: K1 <= W, all PPT steps when W == PPT): issued, not waited for.
 template <int PPT, int K0, int K1>
 __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int lane, int wave,
-                                           u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3])
+                                           u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], bool sys = false)
 {
     static_assert(K1 <= (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT), "steps beyond the window");
     const StepGeom sg = step_geom(lane);
     const uint32_t base = j * (BLOCK * PPT);
     const uint32_t last = B.n ? B.n - 1 : 0u;
 #pragma unroll
-    for (int k = K0; k < K1; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
+    for (int k = K0; k < K1; k++)
+        load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k], sys);
 }
 
 // v: the tile's first W steps as steps_load issued them.
@@ -265,15 +266,15 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
         if (k + W < PPT) load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W]);
         const uint32_t pk0 = base + k * BLOCK;
         const bool valid[1] = {pk0 + tid < B.n && B.n != 0};
-        uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], lpe2[1], src[1], dst[1], ct = 0, cn = 0;
+        uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1], ct = 0, cn = 0;
         if (COPK_XP & 1) {
             verdict[0] = (w3[0] ^ w6[0] ^ w7[0] ^ w8[0]) & 1u;
             port[0] = w7[0] & 3u;
             flags[0] = 0;
             rnh[0] = w8[0];
         } else {
-            pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2);
-            pass2<FW, LPM, 1>(p, w3, src, dst, valid, fwe, lpe, lpe2, verdict, flags, rnh, ct, cn);
+            pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2, fwe2);
+            pass2<FW, LPM, 1>(p, w3, src, dst, valid, fwe, lpe, lpe2, fwe2, verdict, flags, rnh, ct, cn);
         }
         const Counts c = wave_counts<FW, 1>(valid, verdict, flags);
         tot.total += c.total;
@@ -344,10 +345,10 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
 // One tile of the poll-mode kernel, step by step: loads, then tile_steps_v.
 template <int FW, int LPM, int PPT, bool WT>
 __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
-                                           int tid, int lane, int wave)
+                                           int tid, int lane, int wave, bool sys = false)
 {
     u32x4 v[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3];
-    steps_load<PPT, 0, (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT)>(B, j, lane, wave, v);
+    steps_load<PPT, 0, (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT)>(B, j, lane, wave, v, sys);
     tile_steps_v<FW, LPM, PPT, WT>(p, lc, B, j, tid, lane, wave, v);
 }
 
@@ -363,7 +364,7 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
 template <int FW, int LPM, int LAY, int PPT, bool EXT, bool WT>
 __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, const LdsCarve &lc, const CopKBatch &B,
                                           uint32_t look_off, uint32_t j, const LookCtx &lk, int tid, int lane, int wave,
-                                          bool sync_tables, size_t hit_tile)
+                                          bool sync_tables, size_t hit_tile, bool sys = false)
 {
     constexpr bool IMIX = LAY == COPK_LAY_IMIX;
     const Tables &tb = lc.tb;
@@ -395,7 +396,8 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
 #else
         u32x4 v[PPT][3];
 #pragma unroll
-        for (int k = 0; k < PPT; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
+        for (int k = 0; k < PPT; k++)
+            load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k], sys);
 #pragma unroll
         for (int k = 0; k < PPT; k++) gather_step(sg, v[k], w3[k], w6[k], w7[k], w8[k]);
 #endif
@@ -404,7 +406,8 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
             const uint32_t ic = min(base + k * BLOCK + tid, last);
-            const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(B.pkts + B.data_off + (size_t)ic * 16u));
+            const u32x4 v = sys ? ld_sys16(sys_rsrc(B.pkts + B.data_off), ic * 16u)
+                                : __builtin_nontemporal_load((const u32x4 *)(B.pkts + B.data_off + (size_t)ic * 16u));
             w3[k] = v.x;
             w6[k] = v.y;
             w7[k] = v.z;
@@ -414,6 +417,18 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
             const uint32_t ic = min(base + k * BLOCK + tid, last);
+            if (sys) {
+                // the offset array and the packet, system-coherent
+                const uint32_t po = (IMIX ? ld_sys4(sys_rsrc(B.offsets), ic * 4u) : ic * B.stride) + B.data_off;
+                const __amdgpu_buffer_rsrc_t rs = sys_rsrc(B.pkts);
+                const u32x4 a = ld_sys16(rs, po + 12u);
+                const u32x2 b = ld_sys8(rs, po + 28u);
+                w3[k] = a.x;
+                w6[k] = a.w;
+                w7[k] = b.x;
+                w8[k] = b.y;
+                continue;
+            }
             const uint8_t *pk;
             if (IMIX) pk = B.pkts + B.offsets[ic] + B.data_off;
             else pk = B.pkts + (size_t)ic * B.stride + B.data_off;
@@ -435,8 +450,8 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
     if (sync_tables) __syncthreads();   // LDS-DMA table staging has landed
 
     // ---- pass 1 (parse, route, LDS searches, tbl24 loads issued) ----
-    uint32_t verdict[PPT], port[PPT], flags[PPT], rnh[PPT], fwe[PPT], lpe[PPT], lpe2[PPT], src[PPT], dst[PPT];
-    pass1<FW, LPM, PPT>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2);
+    uint32_t verdict[PPT], port[PPT], flags[PPT], rnh[PPT], fwe[PPT], lpe[PPT], lpe2[PPT], fwe2[PPT], src[PPT], dst[PPT];
+    pass1<FW, LPM, PPT>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2, fwe2);
     if (o.dbg & 8u) {
         uint32_t x = 0;
 #pragma unroll
@@ -447,7 +462,7 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
 
     // ---- pass 2 (tbl8 step) and the verdicts ----
     Counts cn;
-    pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, lpe2, verdict, flags, rnh, cn.total, cn.notv4);
+    pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, lpe2, fwe2, verdict, flags, rnh, cn.total, cn.notv4);
     const bool bins = EXT && FW != COPK_TBL_OFF && p.hit_region != nullptr;
     // segmented lists with no optional feature: the lean epilogue (counters
     // from ballots, folded into the list's barriers)

@@ -241,6 +241,12 @@ typedef struct cop_ctx cop_ctx;
  * 16-byte load of two (start, value) pairs decides almost every lookup.
  * Results are identical; takes precedence over COP_CFG_LPM_TRIE. */
 #define COP_CFG_LPM_BKT         0x100u
+/* Firewall tables too large for LDS (config 5's 1M rules) in the same
+ * bucketed interval form, keyed by rule id, instead of the DIR-24-8 image:
+ * about 16 + 12 MiB per 1M rules against 64 MiB, two dependent L2 / Infinity
+ * Cache reads per lookup instead of one random 64 MiB probe. Results, rule
+ * ids and per-rule counters are identical. */
+#define COP_CFG_FW_BKT          0x200u
 #define COP_MAX_DEMUX_PORTS     8
 
 typedef struct cop_config {
@@ -447,14 +453,14 @@ int cop_pmd_stop(cop_pmd *pmd);
  * another agent (the host with cop_memcpy_h2d, a NIC, another GPU) between
  * its batches. A persistent kernel gets no dispatch-time cache invalidation,
  * so a CU or L2 could serve a slot's previous contents. By DEFAULT (no flag,
- * and always through cop_pmd_start) every tile acquires at system scope
- * before it loads its packets once its ring has wrapped in the running
- * launch: a slot's first read in a launch is fresh, every reuse is safe.
- * COP_PMD_SYS_ACQUIRE: acquire on every tile (rings in host memory get this
- * without the flag). COP_PMD_STATIC_SLOTS: the caller declares the slots
- * written once before cop_pmd_start_rings and never again while the kernel
- * runs (a benchmark's resident pool): no acquire. The two contradict
- * (-EINVAL). */
+ * and always through cop_pmd_start) every tile reads its packets with
+ * system-coherent loads (no cached copy used) once its ring has wrapped in
+ * the running launch: a slot's first read in a launch is fresh, every reuse
+ * is safe. COP_PMD_SYS_ACQUIRE: coherent loads on every tile (rings in host
+ * memory get this without the flag). COP_PMD_STATIC_SLOTS: the caller
+ * declares the slots written once before cop_pmd_start_rings and never again
+ * while the kernel runs (a benchmark's resident pool): plain loads. The two
+ * contradict (-EINVAL). */
 #define COP_PMD_SYS_ACQUIRE 2u
 #define COP_PMD_STATIC_SLOTS 4u
 int cop_pmd_start_rings(cop_ctx *ctx, const cop_batch_ring *rings, uint32_t n_rings, uint32_t flags,
@@ -550,6 +556,14 @@ int  cop_coll_reduce_counters(cop_ctx *ctx, cop_counters *total, uint64_t *rule_
 
 /* Device memory helpers so C callers need no HIP headers. */
 int  cop_dev_alloc(cop_ctx *ctx, size_t bytes, void **dptr);
+/* HBM with another cache policy, for a poll-mode ring's outputs (records,
+ * lists, counts) that the host or another agent reads while the kernel runs:
+ * COP_ALLOC_UNCACHED (no GPU cache holds a line: a store is in memory once
+ * it has drained) or COP_ALLOC_FINEGRAINED (coherent fine-grained memory).
+ * Free with cop_dev_free. 0, or -errno. */
+#define COP_ALLOC_UNCACHED 1u
+#define COP_ALLOC_FINEGRAINED 2u
+int  cop_dev_alloc_ex(cop_ctx *ctx, size_t bytes, uint32_t flags, void **dptr);
 int  cop_dev_free(cop_ctx *ctx, void *dptr);
 int  cop_host_alloc_pinned(cop_ctx *ctx, size_t bytes, void **hptr);
 int  cop_host_free_pinned(cop_ctx *ctx, void *hptr);

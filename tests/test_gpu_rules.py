@@ -101,17 +101,25 @@ def test_rule_counters_off_by_default(gpu_ctx_factory):
         ctx.rule_counters()
 
 
-@pytest.mark.parametrize("form", ["dir", "trie", "bkt"])
+C5_FORMS = {"dir": 0, "trie": cg.CFG_LPM_TRIE, "bkt": cg.CFG_LPM_BKT,
+            # the 1M-rule firewall in the bucketed form too (COP_CFG_FW_BKT),
+            # beside a bucketed or a DIR-24-8 route table
+            "fwbkt": cg.CFG_FW_BKT | cg.CFG_LPM_BKT, "fwbkt_rtdir": cg.CFG_FW_BKT}
+
+
+@pytest.mark.parametrize("form", list(C5_FORMS))
 def test_config5_scale_1m_rules_1m_prefixes(gpu_ctx_factory, form):
     """BASELINE configs[4] tables at full size, one 256k batch, full parity;
-    the 1M-prefix route table as DIR-24-8 or as the multibit trie."""
+    the 1M-prefix route table as DIR-24-8, the multibit trie or the bucketed
+    intervals, and the 1M-rule firewall as DIR-24-8 or bucketed intervals
+    keyed by rule id (rule ids, verdicts and per-rule counters identical)."""
     cid = 5
     fw_rules = cg.gen_rules(0x5EED1000 + cid, 1000000, cg.GEN_FW, 0)
     routes = cg.gen_rules(0x5EED2000 + cid, 1000000, cg.GEN_ROUTES, 0)
     fwt = cg.LpmTable(fw_rules, 1000000, 1 << 20, False)
     rtt = cg.LpmTable(routes, 1000000, 1 << 20, False)
     ctx = gpu_ctx_factory(stages=S | F | L, max_batch=262144,
-                          flags=cg.CFG_RULE_COUNTERS | {"dir": 0, "trie": cg.CFG_LPM_TRIE, "bkt": cg.CFG_LPM_BKT}[form])
+                          flags=cg.CFG_RULE_COUNTERS | C5_FORMS[form])
     ctx.set_fw_table(fwt)
     ctx.set_route_lpm(rtt)
     ofw = orc.OracleLpm(1000000, 1 << 20, rules_only=True)

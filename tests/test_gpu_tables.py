@@ -23,7 +23,10 @@ DIR = cg.CFG_FW_FORCE_DIR24 | cg.CFG_LPM_FORCE_DIR24
 # trie: the route stage in its multibit-trie form (LDS top level + L2 nodes);
 # bkt: in its bucketed interval form (index + (start, value) pairs in L2)
 MODES = {"auto": (0, "plain"), "forced": (DIR, "plain"), "packed": (DIR, "packed"),
-         "trie": (cg.CFG_LPM_TRIE, "plain"), "bkt": (cg.CFG_LPM_BKT, "plain")}
+         "trie": (cg.CFG_LPM_TRIE, "plain"), "bkt": (cg.CFG_LPM_BKT, "plain"),
+         # the firewall's table in the bucketed form too (COP_CFG_FW_BKT)
+         "fwbkt": (cg.CFG_LPM_BKT | cg.CFG_FW_BKT, "plain")}
+ROUTE_FORM = {"trie": "trie", "bkt": "bkt", "fwbkt": "bkt"}
 
 
 def dense_routes():
@@ -54,7 +57,7 @@ def test_large_fw_and_routes(gpu_ctx_factory, mode, monkeypatch):
     ctx = gpu_ctx_factory(stages=S | F | L, flags=MODES[mode][0] | cg.CFG_RULE_COUNTERS)
     ctx.set_fw_table(fwt)
     ctx.set_route_lpm(rtt)
-    assert ctx.route_form() == {"trie": "trie", "bkt": "bkt"}.get(mode, "dir")
+    assert ctx.route_form() == ROUTE_FORM.get(mode, "dir")
     ofw = orc.OracleLpm(20000, 1 << 16)
     ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=False)
     ort = orc.OracleLpm(1 << 20, 1 << 16)
@@ -90,7 +93,7 @@ def test_large_table_all_addresses_of_a_dense_chunk(gpu_ctx_factory, mode, monke
     rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
     ctx = gpu_ctx_factory(stages=S | L, flags=MODES[mode][0])
     ctx.set_route_lpm(rtt)
-    assert ctx.route_form() == {"trie": "trie", "bkt": "bkt"}.get(mode, "dir")
+    assert ctx.route_form() == ROUTE_FORM.get(mode, "dir")
     ort = orc.OracleLpm(1 << 20, 1 << 16)
     ort.setup(routes["ip"], routes["depth"], routes["next_hop"], stop_at_error=False)
     n = 65536
@@ -146,3 +149,43 @@ def test_bkt_wide_bucket_on_device(gpu_ctx_factory):
     res = dr.download(cg.RESULT_DT, n)
     for f in ("verdict", "flags", "port", "route_nh"):
         assert np.array_equal(res[f], ro[f]), f"poll mode {f}"
+
+
+def test_fw_bkt_poll_mode_with_rule_counters(gpu_ctx_factory):
+    """The bucketed firewall (COP_CFG_FW_BKT) in the poll-mode kernel: a 20k
+    rule table (out of LDS) with per-rule counters, FW + bucketed route
+    stage, batches posted past the ring's slots: records, lists, counters and
+    per-rule hits equal the oracle's."""
+    fw_rules = cg.gen_rules(0x5EED1078, 20000, cg.GEN_FW, 0)
+    routes = dense_routes()
+    fwt = cg.LpmTable(fw_rules, 20000, 1 << 16, False)
+    rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
+    ctx = gpu_ctx_factory(stages=S | F | L, flags=cg.CFG_FW_BKT | cg.CFG_LPM_BKT | cg.CFG_RULE_COUNTERS)
+    ctx.set_fw_table(fwt)
+    ctx.set_route_lpm(rtt)
+    ofw = orc.OracleLpm(20000, 1 << 16)
+    ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=False)
+    ort = orc.OracleLpm(1 << 20, 1 << 16)
+    ort.setup(routes["ip"], routes["depth"], routes["next_hop"], stop_at_error=False)
+    B, P, N = 65536, 3, 7
+    pk = cg.gen_trace(0x5EED0080, B * P, fw_rules, routes)
+    dp = ctx.alloc(pk.nbytes)
+    dp.upload(pk)
+    dr = ctx.alloc(B * P * 8)
+    df = ctx.alloc(B * P * 4)
+    dc = ctx.alloc(P * 4 + 16)
+    ring = cg.make_ring(dp, P, B, dr, B * 64, fwd_idx=df, fwd_count=dc)
+    ctx.counters(reset=True)
+    with ctx.pmd_start(ring) as m:
+        m.run(N)
+    res = dr.download(cg.RESULT_DT, B * P)
+    fwd = df.download(np.uint32, B * P)
+    cnt = dc.download(np.uint32, P)
+    hits = np.zeros(ofw.n_rules, np.uint64)
+    for s in range(P):
+        h = np.zeros(ofw.n_rules, np.uint64)
+        ro, fo, _ = orc.process(pk[s * B * 64:(s + 1) * B * 64], B, stages=S | F | L, fw=ofw, route=ort, rule_hits=h)
+        assert_parity(res[s * B:(s + 1) * B], fwd[s * B:s * B + int(cnt[s])], ro, fo)
+        hits += h * np.uint64(len(range(s, N, P)))   # slot s served batches s, s + P, ...
+    assert ctx.counters()["rx"] == N * B
+    assert np.array_equal(ctx.rule_counters(), hits)

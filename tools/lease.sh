@@ -62,10 +62,10 @@ for s in "$@"; do
       step 300 "$out/c5_${C5_FORM:-dir}.log" $B --quick --workload fw_lpm_1m --steps 20 --warmup 5 --route-form "${C5_FORM:-dir}" $BENCH_ARGS
       line "$out/c5_${C5_FORM:-dir}.log" ;;
     c5_forms)
-      for f in "dir dir" "dir bkt" "bkt bkt"; do
+      for f in "dir dir" "dir bkt" "bkt bkt" "bkt dir"; do
         set -- $f
-        COP_FW_FORM=$1 step 300 "$out/c5_fw$1_rt$2.log" $B --quick --workload fw_lpm_1m --steps 20 --warmup 5 --route-form "$2" $BENCH_ARGS
-        echo "fw $1 route $2: $(line "$out/c5_fw$1_rt$2.log" | cut -c1-200)"
+        step 300 "$out/c5_fw$1_rt$2.log" $B --quick --workload fw_lpm_1m --steps 20 --warmup 5 --fw-form "$1" --route-form "$2" $BENCH_ARGS
+        grep -h '^{"metric"' "$out/c5_fw$1_rt$2.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print("fw", sys.argv[1], "route", sys.argv[2], d["value"], "kernel frac", r["frac"], "ms/launch", r["kernel_ms_per_launch"], "timed", r["frac_timed"])' "$1" "$2"
       done ;;
     imix)
       step 300 "$out/imix20.log" $B --quick --workload fw_lpm_imix --steps 20 --warmup 5 $BENCH_ARGS
@@ -84,9 +84,34 @@ for s in "$@"; do
         i=$((i + 1))
         COP_PMD_DYN=$v step 300 "$out/dyn${v}_$i.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS
         grep -h '^{"metric"' "$out/dyn${v}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("dyn", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$v"
+      done ;;
+    acq)
+      # slot-reuse modes at the driver's 20 steps ($COP_PMD_ACQUIRE: 0 none,
+      # 1 acquire every tile, 3 coherent loads every tile), then the
+      # rewritten-slot tests with coherent loads every tile / once wrapped
+      for v in 0 1 3 4 0 1 3 4; do
+        COP_PMD_ACQUIRE=$v step 200 "$out/acq$v.log" $B --quick --steps 20 --warmup 5 --repeats 11 $BENCH_ARGS
+        echo "acq=$v $(grep -h '^\[rank 0\] fw1k: timed' "$out/acq$v.log" | cut -c1-120)"
       done
-      for v in 0 1; do
-        COP_PMD_DYN=$v step 300 "$out/dyn_steady$v.log" python3 -u "$R/tools/pmd_probe.py"
+      for v in 3 4; do
+        COP_PMD_ACQUIRE=$v step 300 "$out/pytest_acq$v.log" python3 -u -m pytest "$R/tests" -m gpu -v -k "rewritten or rings or pmd_seg" --timeout 120 --timeout-method thread
+        grep -E "FAILED|ERROR|passed|failed" "$out/pytest_acq$v.log" | tail -4
+      done ;;
+    reuse)
+      # the default slot-reuse guard against declared-static slots, with the
+      # poll-mode steady state (1024-batch posts wrap the 1024-slot pool)
+      for v in static reuse static reuse; do
+        step 300 "$out/reuse_$v.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check --slots $v $BENCH_ARGS
+        grep -h '^{"metric"' "$out/reuse_$v.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("slots", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$v"
+      done ;;
+    outmem)
+      # outputs in uncached / fine-grained HBM with plain (not write-through)
+      # stores (libcopgpu_wt0.so: -DCOPK_PMD_WT=0) against HBM + write-through
+      for v in device:main uncached:wt0 fine:wt0 device:main uncached:wt0; do
+        mem=${v%%:*}; lib=${v##*:}
+        L=""; [ "$lib" = wt0 ] && L="$R/ghost-dataplane_amd/libcopgpu_wt0.so"
+        COP_LIB=$L step 300 "$out/outmem_$mem.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check --out-mem $mem $BENCH_ARGS
+        grep -h '^{"metric"' "$out/outmem_$mem.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("out", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$v"
       done ;;
     pytest_dyn)
       COP_PMD_DYN=1 step 600 "$out/pytest_dyn.log" python3 -u -m pytest "$R/tests" -m gpu -v -k "pmd or seg or rings or dropin" --timeout 120 --timeout-method thread
