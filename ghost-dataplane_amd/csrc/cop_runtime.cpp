@@ -2507,6 +2507,10 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
         // binned hits: leave room beside the workers for the count kernel
         // (64 KiB of LDS and a workgroup per CU)
         if (m->bins) occ = std::min(occ, 4);
+        // dynamic tiles: leave a workgroup slot per CU free (at six workers
+        // per CU a pageable cop_memcpy_h2d beside the kernel waited for its
+        // idle exit: profiles/r05/check1/pytest_dyn.log, relaunches per post)
+        if (m->dyn) occ = std::min(occ, 5);
         if (const char *env = getenv("COP_PMD_PER_CU")) occ = std::min(occ, std::max(1, atoi(env)));
         m->per_cu = (uint32_t)occ;
         pmd_size(m);
