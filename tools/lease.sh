@@ -113,6 +113,17 @@ for s in "$@"; do
         COP_LIB=$L step 300 "$out/outmem_$mem.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check --out-mem $mem $BENCH_ARGS
         grep -h '^{"metric"' "$out/outmem_$mem.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("out", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$v"
       done ;;
+    tail)
+      step 300 "$out/tail.log" python3 -u "$R/tools/pmd_tail.py" --posts 60 --dump "$out/tail.npz"
+      cat "$out/tail.log" ;;
+    rings_ab)
+      # the poll-mode drop-in loops: coherent loads on every tile (3, the
+      # default for host rings) against an acquire on every tile (1)
+      for v in 3 1 3 1; do
+        COP_PMD_ACQUIRE=$v step 120 "$out/ring5_pmd_acq$v.log" "$R/tools/ringbench" 8388608 16384 5 pmd
+        COP_PMD_ACQUIRE=$v step 90 "$out/ring1_pmd_acq$v.log" "$R/tools/ringbench" 8388608 16384 1 pmd
+        echo "acq=$v $(grep -h aggregate "$out/ring5_pmd_acq$v.log") / $(grep -h aggregate "$out/ring1_pmd_acq$v.log")"
+      done ;;
     pytest_dyn)
       COP_PMD_DYN=1 step 600 "$out/pytest_dyn.log" python3 -u -m pytest "$R/tests" -m gpu -v -k "pmd or seg or rings or dropin" --timeout 120 --timeout-method thread
       grep -E "FAILED|ERROR|passed|failed" "$out/pytest_dyn.log" | tail -6 ;;
