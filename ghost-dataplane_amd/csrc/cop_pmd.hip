@@ -393,11 +393,12 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
     };
     // Dynamic tiles (P.dyn, step-by-step tiles only: segmented lists need no
     // look-back, so any worker may take any tile and none ever waits on
-    // another). A worker claims tiles from its ring's ticket counter, one
-    // ahead: while it classifies and stores tile T, the header loads of its
-    // next tile Tn (claimed one tile earlier) are already in flight, and the
-    // claim of the tile after that too. Once T's stores, counter adds and
-    // those loads have drained (one vmcnt(0)), T is counted for its slot;
+    // another). A worker claims tiles from its ring's ticket counters: once
+    // tile T's batch is posted and its loads are issued, it claims its next
+    // tile Tn, and when Tn's batch is posted too, Tn's header loads go out
+    // before T is classified and stored, so they are in flight during T's
+    // work. Once T's stores, counter adds and those loads have drained (one
+    // vmcnt(0)), T is counted for its slot;
     // that returning add is read one tile later (or before the worker waits
     // for a post), so no round trip stands between two tiles. Workers the
     // memory system serves first simply take more tiles: no static tail.
@@ -405,9 +406,12 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
     // above the closed gate's count; tickets are claimed in order, so every
     // tile of every batch below the gate was claimed by a worker that serves
     // it. A relaunch zeroes the tickets (ticket 0 = tile 0 of batch seq0r).
+    constexpr bool DYN_OK = PPT <= 2 || (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT) <= 2;
     auto serve_dyn = [&](auto steps_c) {
-        // (two tiles' loads live at once: 256- and 512-packet tiles only)
-        constexpr bool STEPS = decltype(steps_c)::value && PPT <= 2;
+        // (two tiles' loads live at once: 256- and 512-packet tiles, or
+        // 1024-packet tiles with a window of at most two steps in flight,
+        // COPK_PMD_WIN <= 2)
+        constexpr bool STEPS = decltype(steps_c)::value && DYN_OK;
         if constexpr (STEPS) {
             constexpr int W = COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT;
             // ticket lanes: one per XCD-sized group of the ring's workers
@@ -437,18 +441,19 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             };
             auto claim = [&] { return __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
             auto tk_get = [&] { return ((unsigned long long)s_tk[1] << 32) | s_tk[0]; };
-            // the first two claims
+            // the first claim. A worker holds one unserved ticket while it
+            // waits for a post and claims its next tile only once the
+            // current one's batch is posted: holding two at the post would
+            // give some workers two tiles of a 20-batch post and others none
+            // (1024-packet tiles: 29 against 46 Gpkt/s at 20 steps,
+            // profiles/r05/check5/)
             if (tid == 0) {
                 const unsigned long long t0 = claim();
-                const unsigned long long t1 = claim();
                 s_tk[0] = (uint32_t)t0;
                 s_tk[1] = (uint32_t)(t0 >> 32);
-                s_tk[2] = (uint32_t)t1;
-                s_tk[3] = (uint32_t)(t1 >> 32);
             }
             lds_barrier();
             unsigned long long T = tk_get();
-            unsigned long long Tn = ((unsigned long long)s_tk[3] << 32) | s_tk[2];
             lds_barrier();
             // two load buffers used in turn (the loop body is instantiated
             // once per buffer order): a tile's loads land in the registers
@@ -506,6 +511,15 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                         steps_load<PPT, 0, W>(pmd_batch(p, rg, slot, n, ntiles), j, lane_i, wave_i, cur, sysld);
                 }
                 if (stamp && tid == 0) st_stamp(&stamp[1], __builtin_amdgcn_s_memrealtime());   // loads issued
+                // T is posted: claim the next tile (its return lands after
+                // T's loads, which this tile waits for anyway)
+                if (tid == 0) {
+                    const unsigned long long tn = claim();
+                    s_tk[0] = (uint32_t)tn;
+                    s_tk[1] = (uint32_t)(tn >> 32);
+                }
+                lds_barrier();
+                const unsigned long long Tn = tk_get();
                 // the next tile's loads, before this tile's work, when its
                 // batch is known posted (fixed-size batches)
                 const unsigned long long bn = seq0 + Tn / per;
@@ -520,9 +534,6 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                     if (jn < ntiles)
                         steps_load<PPT, 0, W>(pmd_batch(p, rg, sn, rg.n, ntiles), jn, lane_i, wave_i, nxt, sysld);
                 }
-                // and the claim after it
-                unsigned long long tnn = 0;
-                if (tid == 0) tnn = claim();
                 if (j < ntiles)
                     tile_steps_v<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, pmd_batch(p, rg, slot, n, ntiles), j, tid_i,
                                                                   lane_i, wave_i, cur);
@@ -543,13 +554,9 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                     pend_b = b;
                     pend_sl = slot;
                     pend = true;
-                    s_tk[0] = (uint32_t)tnn;
-                    s_tk[1] = (uint32_t)(tnn >> 32);
                     if (stamp) st_stamp(&stamp[3], __builtin_amdgcn_s_memrealtime());   // counted
                 }
-                lds_barrier();
                 T = Tn;
-                Tn = tk_get();
                 loaded = pf;
                 return false;
             };
@@ -561,7 +568,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         }
     };
     if (steps_ok<FW, LPM, LAY, EXT>() && p.seg && p.compact && p.rec_paired && P.stepwise) {
-        if (PPT <= 2 && P.dyn) serve_dyn(std::integral_constant<bool, steps_ok<FW, LPM, LAY, EXT>()>{});
+        if (DYN_OK && P.dyn) serve_dyn(std::integral_constant<bool, steps_ok<FW, LPM, LAY, EXT>()>{});
         else serve(std::integral_constant<bool, steps_ok<FW, LPM, LAY, EXT>()>{});
     } else {
         serve(std::integral_constant<bool, false>{});

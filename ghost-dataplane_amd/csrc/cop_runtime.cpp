@@ -2407,9 +2407,10 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
     // dynamic tiles ($COP_PMD_DYN=1; segmented lists, step-by-step tiles):
     // claimed one ahead with the next tile's loads in flight, so 256-packet
     // tiles (two tiles' loads in registers fit the 6-worker budget)
+    // ($COP_PMD_DYN=4: 1024-packet tiles, for builds with COPK_PMD_WIN <= 2)
     const char *dyn_env = getenv("COP_PMD_DYN");
     m->dyn = dyn_env && atoi(dyn_env) != 0 && seg;
-    if (m->dyn) ppt = 1;
+    if (m->dyn) ppt = atoi(dyn_env) == 4 ? 4 : 1;
     if (c->ppt_override) ppt = c->ppt_override;
     pl.ppt = ppt;
     m->ppt = ppt;

@@ -418,3 +418,50 @@ def test_coprocessor_poll_pmd_rings(rules_file):
         assert res == [(True, True, True)] * R, res
     finally:
         L.coprocessor_teardown()
+
+
+def test_pmd_host_odd_max_pkts_equal_to_max_batch(rules_file, gpu_ctx_factory):
+    """cop_pmd_host_create with an odd max_pkts equal to the
+    context's max_batch. The ring's batches hold max_pkts packets (its
+    slots are max_pkts rounded up to even apart), so the start no longer
+    fails with 'n > max_batch'; one full drain of max_pkts packets comes
+    back in the oracle's forward order, its drops freed."""
+    path, rules = rules_file
+    L = cg.lib()
+    L.cop_set_mbuf_layout(0, 16)
+    n = 4097
+    ctx = gpu_ctx_factory(stages=cg.STAGE_FW, max_batch=n)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    hp = ctypes.c_void_p()
+    assert L.cop_pmd_host_create(ctx.handle, 1, n, 2, ctypes.byref(hp)) == 0
+    try:
+        fwo, _ = oracle_tables(rules)
+        pk = cg.gen_trace(0x5EED0630, n, rules)
+        mb = Mbufs(pk, n)
+        _, fo, _ = orc.process(pk, n, stages=DROPIN, fw=fwo)
+        rx = L.cop_ring_create(16384)
+        tx = L.cop_ring_create(16384)
+        FREE = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)
+        freed = []
+        cb = FREE(lambda m, arg: freed.append(mb.index(m)))
+        stats = cg.NfStats()
+        for s in range(0, n, 32):
+            k = min(32, n - s)
+            arr = (ctypes.c_void_p * k)(*[mb.ptr(j) for j in range(s, s + k)])
+            assert L.cop_ring_enqueue_bulk(rx, arr, k, None) == k
+        got = L.cop_coprocessor_poll_pmd(hp, 0, rx, tx, n, cb, None, ctypes.byref(stats))
+        assert got >= 0, got
+        assert L.cop_coprocessor_flush_pmd(hp, 0, tx, cb, None, ctypes.byref(stats)) >= 0
+        buf = (ctypes.c_void_p * 256)()
+        out = []
+        while True:
+            k = L.cop_ring_dequeue_burst(tx, buf, 256, None)
+            if not k:
+                break
+            out += [mb.index(buf[i]) for i in range(k)]
+        assert out == list(fo)
+        assert sorted(freed) == sorted(set(range(n)) - set(fo))
+        L.cop_ring_free(rx)
+        L.cop_ring_free(tx)
+    finally:
+        assert L.cop_pmd_host_destroy(hp) == 0

@@ -124,6 +124,19 @@ for s in "$@"; do
         COP_PMD_ACQUIRE=$v step 90 "$out/ring1_pmd_acq$v.log" "$R/tools/ringbench" 8388608 16384 1 pmd
         echo "acq=$v $(grep -h aggregate "$out/ring5_pmd_acq$v.log") / $(grep -h aggregate "$out/ring1_pmd_acq$v.log")"
       done ;;
+    dyn4)
+      # dynamic 1024-packet tiles with a two-step window (libcopgpu_win2.so,
+      # -DCOPK_PMD_WIN=2, $COP_PMD_DYN=4) against the static order in the
+      # same build and in the default build
+      i=0
+      for v in main:0 win2:0 win2:4 main:0 win2:0 win2:4; do
+        i=$((i + 1)); lib=${v%%:*}; d=${v##*:}
+        L=""; [ "$lib" = win2 ] && L="$R/ghost-dataplane_amd/libcopgpu_win2.so"
+        COP_LIB=$L COP_PMD_DYN=$d step 300 "$out/dyn4_${lib}_${d}_$i.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS
+        grep -h '^{"metric"' "$out/dyn4_${lib}_${d}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("dyn4", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"), p.get("workers"))' "$v"
+      done
+      COP_LIB="$R/ghost-dataplane_amd/libcopgpu_win2.so" COP_PMD_DYN=4 step 600 "$out/pytest_dyn4.log" python3 -u -m pytest "$R/tests" -m gpu -v -k "pmd or seg or rings" --timeout 120 --timeout-method thread
+      grep -E "FAILED|ERROR|passed|failed" "$out/pytest_dyn4.log" | tail -4 ;;
     pytest_dyn)
       COP_PMD_DYN=1 step 600 "$out/pytest_dyn.log" python3 -u -m pytest "$R/tests" -m gpu -v -k "pmd or seg or rings or dropin" --timeout 120 --timeout-method thread
       grep -E "FAILED|ERROR|passed|failed" "$out/pytest_dyn.log" | tail -6 ;;
