@@ -459,6 +459,29 @@ def measure(args, name, rank, world, dev, group, gate, primary):
         t_one = time.perf_counter() - t0
         info = pmd.info()
         t_long = float(np.median(longs))
+        # the same posts with dynamic tiles (COP_PMD_DYNAMIC_TILES, segmented
+        # lists): a kernel of its own, the 1024-batch steady state and the
+        # driver's 20-step post (reported beside the static order's)
+        dyn = None
+        if seg:
+            pmd_off()
+            pmd = ctx.pmd_start(ring, pmd_flags | cg.PMD_DYNAMIC_TILES)
+            pmd.run(n_long)
+            d_longs, d_short = [], []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                pmd.run(n_long)
+                d_longs.append(time.perf_counter() - t0)
+            for _ in range(11):
+                t0 = time.perf_counter()
+                pmd.run(args.steps)
+                d_short.append(time.perf_counter() - t0)
+            di = pmd.info()
+            dl = float(np.median(d_longs))
+            dyn = {"workers": di["workers"], "packets_per_tile": di["packets_per_tile"],
+                   "steady_mpkt_s": round(n_long * B / dl / 1e6, 3), "steady_ms": round(dl * 1e3, 4),
+                   f"mpkt_s_{args.steps}_steps": round(args.steps * B / float(np.median(d_short)) / 1e6, 3),
+                   "note": "not the line's value: host-timed posts of this kernel, no gate"}
         res["pmd_info"] = {"workers": info["workers"], "workers_per_cu": info["workers_per_cu"],
                            "packets_per_tile": info["packets_per_tile"], "launches": info["launches"],
                            "steady_batches": n_long, "steady_mpkt_s": round(n_long * B / t_long / 1e6, 3),
@@ -466,6 +489,8 @@ def measure(args, name, rank, world, dev, group, gate, primary):
                            "single_batch_post_to_done_us_median": round(float(np.median(lat)), 2),
                            "one_batch_posts": {"batches": n_one, "in_flight": depth,
                                                "mpkt_s": round(n_one * B / t_one / 1e6, 3)}}
+        if dyn:
+            res["pmd_info"]["dynamic_tiles"] = dyn
     pmd_off()
 
     if rc_on and coll == "ok":
@@ -831,6 +856,9 @@ def main():
         # launch) timed on the host, as a fraction of the peak
         pi = res["pmd_info"]
         pi["steady_frac"] = round(pi["steady_mpkt_s"] * 1e6 * res["bytes_per_pkt"] / 1e9 / HBM_PEAK_GBS, 4)
+        if "dynamic_tiles" in pi:
+            dt = pi["dynamic_tiles"]
+            dt["steady_frac"] = round(dt["steady_mpkt_s"] * 1e6 * res["bytes_per_pkt"] / 1e9 / HBM_PEAK_GBS, 4)
         out["pmd"] = pi
         # the roofline of the engine that produced `value` when it is the
         # poll-mode kernel: algorithmic bytes of its steady 1024-batch post

@@ -659,7 +659,8 @@ class Context:
 
 PMD_VARIABLE_N = 1
 PMD_SYS_ACQUIRE = 2     # acquire on every tile
-PMD_STATIC_SLOTS = 4    # slots written once before the start: no acquire (default: acquire once the ring wraps)
+PMD_STATIC_SLOTS = 4    # slots written once before the start: plain loads (default: coherent loads once the ring wraps)
+PMD_DYNAMIC_TILES = 8   # tiles claimed from tickets, the next tile's loads issued early (segmented lists)
 
 
 class Pmd:

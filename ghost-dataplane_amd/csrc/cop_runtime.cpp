@@ -2363,7 +2363,7 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
     if (!c || !rings || !out || n_rings < 1) return -EINVAL;
     *out = nullptr;
     if (n_rings > COPK_PMD_MAX_RINGS) return set_err(c, -EINVAL, "pmd: %u rings > %d", n_rings, COPK_PMD_MAX_RINGS);
-    if (flags & ~(COP_PMD_VARIABLE_N | COP_PMD_SYS_ACQUIRE | COP_PMD_STATIC_SLOTS))
+    if (flags & ~(COP_PMD_VARIABLE_N | COP_PMD_SYS_ACQUIRE | COP_PMD_STATIC_SLOTS | COP_PMD_DYNAMIC_TILES))
         return set_err(c, -EINVAL, "pmd: unknown flags %#x", flags);
     if ((flags & COP_PMD_SYS_ACQUIRE) && (flags & COP_PMD_STATIC_SLOTS))
         return set_err(c, -EINVAL, "pmd: COP_PMD_SYS_ACQUIRE and COP_PMD_STATIC_SLOTS contradict");
@@ -2404,13 +2404,13 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
     // of 64k packets is one tile per worker), 256-packet tiles for small
     // batches
     int ppt = r->n >= 4u * COPK_BLOCK * 4 ? 4 : 1;
-    // dynamic tiles ($COP_PMD_DYN=1; segmented lists, step-by-step tiles):
-    // claimed one ahead with the next tile's loads in flight, so 256-packet
-    // tiles (two tiles' loads in registers fit the 6-worker budget)
-    // ($COP_PMD_DYN=4: 1024-packet tiles, for builds with COPK_PMD_WIN <= 2)
+    // dynamic tiles (COP_PMD_DYNAMIC_TILES; segmented lists, step-by-step
+    // tiles): the next tile's first two steps' loads in flight during the
+    // current one (COPK_PMD_WIN 2). A/B runs: $COP_PMD_DYN=1 256-packet
+    // dynamic tiles, 4 the flag's 1024-packet tiles, 0 off
     const char *dyn_env = getenv("COP_PMD_DYN");
-    m->dyn = dyn_env && atoi(dyn_env) != 0 && seg;
-    if (m->dyn) ppt = atoi(dyn_env) == 4 ? 4 : 1;
+    m->dyn = seg && (dyn_env ? atoi(dyn_env) != 0 : (flags & COP_PMD_DYNAMIC_TILES) != 0);
+    if (m->dyn && dyn_env && atoi(dyn_env) == 1) ppt = 1;
     if (c->ppt_override) ppt = c->ppt_override;
     pl.ppt = ppt;
     m->ppt = ppt;

@@ -206,8 +206,12 @@ constexpr bool steps_ok()
 #ifndef COPK_XP
 #define COPK_XP 0
 #endif
+// Steps of a tile whose header loads are in flight at once: two. Against
+// four, the driver's 20-batch post ran 45.8-47.2 vs 44.4-45.4 Gpkt/s in four
+// alternating pairs on two boxes (profiles/r05/check5/, check6/), and two
+// leave room for the next tile's first two steps (dynamic tiles)
 #ifndef COPK_PMD_WIN
-#define COPK_PMD_WIN 4
+#define COPK_PMD_WIN 2
 #endif
 // the step's forward-list segment through LDS and out as 16-byte stores
 #ifndef COPK_PMD_STAGE_LIST

@@ -463,6 +463,12 @@ int cop_pmd_stop(cop_pmd *pmd);
  * contradict (-EINVAL). */
 #define COP_PMD_SYS_ACQUIRE 2u
 #define COP_PMD_STATIC_SLOTS 4u
+/* Dynamic tiles (rings with segmented lists, COP_CFG_SEG_LISTS): workers
+ * claim tiles from ticket counters instead of a static order, and issue the
+ * next tile's header loads before they classify the current one. Same
+ * outputs; a higher poll-mode steady state on long streams, about the same
+ * rate on short bursts. Ignored without segmented lists. */
+#define COP_PMD_DYNAMIC_TILES 8u
 int cop_pmd_start_rings(cop_ctx *ctx, const cop_batch_ring *rings, uint32_t n_rings, uint32_t flags,
                         cop_pmd **out);
 /* Post the next `count` full batches (n packets each) of one ring. */

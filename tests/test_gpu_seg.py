@@ -208,10 +208,13 @@ class SegRing:
         return res
 
 
-def test_pmd_seg_posts_wrap(gpu_ctx_factory):
+@pytest.mark.parametrize("flags", [0, cg.PMD_DYNAMIC_TILES])
+def test_pmd_seg_posts_wrap(gpu_ctx_factory, flags):
     """The bench's engine and shape: a 20-batch post (one tile per worker),
     then posts that wrap the ring; counters read beside the running kernel
-    see every completed batch."""
+    see every completed batch. In the static tile order and with dynamic
+    tiles (COP_PMD_DYNAMIC_TILES: claimed from tickets, the next tile's
+    loads issued early)."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
@@ -219,7 +222,7 @@ def test_pmd_seg_posts_wrap(gpu_ctx_factory):
     B, P = 65536, 24
     pk = cg.gen_trace(0x5EED5E20, B * P, rules)
     rg = SegRing(ctx, pk, B, P)
-    with ctx.pmd_start(rg.ring) as m:
+    with ctx.pmd_start(rg.ring, flags) as m:
         m.post(20)
         m.wait()
         assert ctx.counters()["rx"] == 20 * B      # read while the kernel runs
@@ -235,11 +238,12 @@ def test_pmd_seg_posts_wrap(gpu_ctx_factory):
     assert ctx.counters()["rx"] == total * B
 
 
-def test_pmd_seg_prefetch_deep_posts(gpu_ctx_factory):
+@pytest.mark.parametrize("flags", [0, cg.PMD_DYNAMIC_TILES])
+def test_pmd_seg_prefetch_deep_posts(gpu_ctx_factory, flags):
     """Posts deeper than one tile per worker: every worker holds several
-    tiles of one post, so each tile prefetches its successor's headers
-    (tile_steps PF) while it finishes; posts of the whole ring, then odd
-    sizes that wrap it, with the outputs cleared in between."""
+    tiles of one post (with dynamic tiles each prefetches its next tile's
+    first steps while it finishes the current one); posts of the whole
+    ring, then odd sizes that wrap it, with the outputs cleared in between."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
@@ -247,7 +251,7 @@ def test_pmd_seg_prefetch_deep_posts(gpu_ctx_factory):
     B, P = 65536, 64
     pk = cg.gen_trace(0x5EED5E64, B * P, rules)
     rg = SegRing(ctx, pk, B, P)
-    with ctx.pmd_start(rg.ring) as m:
+    with ctx.pmd_start(rg.ring, flags) as m:
         assert m.info()["workers"] * 3 < P * m.info()["tiles_per_batch"]
         m.post(P)
         m.wait()
@@ -304,13 +308,14 @@ def test_pmd_live_snapshots_sum_exactly(gpu_ctx_factory):
     assert np.array_equal(hits_sum, want)
 
 
-@pytest.mark.parametrize("flags", [0, cg.CFG_SEG_LISTS])
-def test_pmd_idle_exit_races_posts(gpu_ctx_factory, monkeypatch, flags):
+@pytest.mark.parametrize("flags,pflags", [(0, 0), (cg.CFG_SEG_LISTS, 0), (cg.CFG_SEG_LISTS, cg.PMD_DYNAMIC_TILES)])
+def test_pmd_idle_exit_races_posts(gpu_ctx_factory, monkeypatch, flags, pflags):
     """A post racing the idle exit: with a 2 ms idle limit the
     host posts at intervals around it, so some posts land while leaders are
     leaving. Every batch must still complete with the oracle's outputs
     (dense lists: no look-back granule of a half-done batch survives the
-    relaunch; segmented: no chain at all)."""
+    relaunch; segmented: no chain at all; dynamic tiles: every ticket below
+    the closed gate is served, the relaunch restarts the tickets)."""
     monkeypatch.setenv("COP_PMD_IDLE_MS", "2")
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=flags)
@@ -324,7 +329,7 @@ def test_pmd_idle_exit_races_posts(gpu_ctx_factory, monkeypatch, flags):
         from test_gpu_pmd import Ring, check, oracle_slots
         rg = Ring(ctx, pk, B, P)
         ro, fos = oracle_slots(pk, B, P, S | F, fw)
-    m = ctx.pmd_start(rg.ring)
+    m = ctx.pmd_start(rg.ring, pflags)
     posted = 0
     for i in range(40):
         time.sleep((1.0 + 0.05 * (i % 41)) * 1e-3 + (0.002 if i % 5 == 4 else 0.0))

@@ -58,6 +58,17 @@ for s in "$@"; do
       step 200 "$out/pmd_pmc_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/pmd_write" -o pmd --output-format csv -- python3 "$R/tools/pmc_pmd.py" run --batches 1024
       step 200 "$out/mb_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/mb_fetch" -o mb --output-format csv -- "$R/tools/membench"
       step 200 "$out/mb_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/mb_write" -o mb --output-format csv -- "$R/tools/membench" ;;
+    pmc_oneshot)
+      # the one-shot kernel's PMC passes over the driver's command (reduce
+      # here with tools/pmc_traffic.py and the membench passes of pmc_pmd)
+      step 300 "$out/os_pmc_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/os_fetch" -o os --output-format csv -- python3 "$R/bench.py" --quick --steps 20 --warmup 5 --secondary none --no-cpu
+      step 300 "$out/os_pmc_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/os_write" -o os --output-format csv -- python3 "$R/bench.py" --quick --steps 20 --warmup 5 --secondary none --no-cpu ;;
+    n2)
+      # two ranks sharing the one GPU (one-shot launches: two persistent
+      # kernels cannot both hold every CU), through the start gate; config
+      # 5's RCCL init fails on a shared GPU and every rank skips the reduce
+      step 600 "$out/n2_shared.log" $B --gpus 2 --allow-shared-gpu --engine launch --steps 20 --warmup 5 --no-cpu --no-rccl-check --secondary fw_lpm_1m
+      grep -h '^{"metric"' "$out/n2_shared.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("n2", d["value"], "overlap", d["windows_overlap"], "union", d["value_union"], "skew", d["windows"]["start_skew_us_median"], "c5", {k: d["secondary"]["fw_lpm_1m"].get(k) for k in ("value", "windows_overlap", "rccl_init", "error")})' ;;
     c5)
       step 300 "$out/c5_${C5_FORM:-dir}.log" $B --quick --workload fw_lpm_1m --steps 20 --warmup 5 --route-form "${C5_FORM:-dir}" $BENCH_ARGS
       line "$out/c5_${C5_FORM:-dir}.log" ;;
