@@ -507,6 +507,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                     if (P.sys_acquire == 1u || (P.sys_acquire == 2u && wrapped))
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                     const bool sysld = P.sys_acquire == 3u || (P.sys_acquire == 4u && wrapped);
+                    step_prio<0>();
                     if (j < ntiles)
                         steps_load<PPT, 0, W>(pmd_batch(p, rg, slot, n, ntiles), j, lane_i, wave_i, cur, sysld);
                 }
@@ -534,9 +535,11 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                     if (jn < ntiles)
                         steps_load<PPT, 0, W>(pmd_batch(p, rg, sn, rg.n, ntiles), jn, lane_i, wave_i, nxt, sysld);
                 }
-                if (j < ntiles)
+                if (j < ntiles) {
+                    const bool sys_t = P.sys_acquire == 3u || (P.sys_acquire == 4u && b >= seq0 + n_slots);
                     tile_steps_v<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, pmd_batch(p, rg, slot, n, ntiles), j, tid_i,
-                                                                  lane_i, wave_i, cur);
+                                                                  lane_i, wave_i, cur, sys_t);
+                }
                 if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done
                 // this tile's stores and counter adds landed (and the next
                 // tile's loads and the claim), then it is counted. The wait

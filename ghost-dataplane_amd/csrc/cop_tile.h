@@ -206,13 +206,30 @@ constexpr bool steps_ok()
 #ifndef COPK_XP
 #define COPK_XP 0
 #endif
-// Steps of a tile whose header loads are in flight at once: two. Against
-// four, the driver's 20-batch post ran 45.8-47.2 vs 44.4-45.4 Gpkt/s in four
-// alternating pairs on two boxes (profiles/r05/check5/, check6/), and two
-// leave room for the next tile's first two steps (dynamic tiles)
+// Steps of a tile whose header loads are in flight at once per wave: one.
+// A CU serves its five workers' requests about in issue order, so the more
+// steps each wave issues up front, the later the CU's last worker gets its
+// data. With one step in flight a wave issues its next
+// step's loads as it gathers the current one, and the workers' requests
+// interleave. The driver's 20-batch post: four steps 44.4-45.4, two
+// 45.8-47.2 (profiles/r05/check5/, check6/), one 51.5-52.2 against two's
+// 46.9-47.3 in three alternating pairs on one box (check8/); the poll-mode
+// steady state is the same. It also leaves room for the next tile's first
+// step (dynamic tiles).
 #ifndef COPK_PMD_WIN
-#define COPK_PMD_WIN 2
+#define COPK_PMD_WIN 1
 #endif
+// experiment builds: wave priority by progress (s_setprio 3 for a tile's
+// first step down to 0 for its last and while waiting), so a CU's lagging
+// waves issue before the ones a step ahead
+#ifndef COPK_PMD_PRIO
+#define COPK_PMD_PRIO 0
+#endif
+template <int K>
+__device__ __forceinline__ void step_prio()
+{
+    if constexpr (COPK_PMD_PRIO) __builtin_amdgcn_s_setprio(K >= 3 ? 0 : 3 - K);
+}
 // the step's forward-list segment through LDS and out as 16-byte stores
 #ifndef COPK_PMD_STAGE_LIST
 #define COPK_PMD_STAGE_LIST 1
@@ -232,11 +249,13 @@ __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int l
         load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k], sys);
 }
 
-// v: the tile's first W steps as steps_load issued them.
+// v: the tile's first W steps as steps_load issued them. sys: the later
+// steps' loads are system-coherent too (as steps_load's were: a reused or
+// host-memory slot, cop_pmd.hip)
 template <int FW, int LPM, int PPT, bool WT, bool STAGE_LIST = COPK_PMD_STAGE_LIST>
 __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
                                              int tid, int lane, int wave,
-                                             u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3])
+                                             u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], bool sys = false)
 {
     static_assert(COPK_SEG == BLOCK, "one segment per tile step");
     const Tables &tb = lc.tb;
@@ -266,8 +285,14 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         uint32_t w3[1], w6[1], w7[1], w8[1];
+        if (COPK_PMD_PRIO) {
+            if (k == 1) step_prio<1>();
+            else if (k == 2) step_prio<2>();
+            else if (k == 3) step_prio<3>();
+        }
         gather_step(sg, v[k % W], w3[0], w6[0], w7[0], w8[0]);
-        if (k + W < PPT) load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W]);
+        if (k + W < PPT)
+            load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W], sys);
         const uint32_t pk0 = base + k * BLOCK;
         const bool valid[1] = {pk0 + tid < B.n && B.n != 0};
         uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1], ct = 0, cn = 0;
@@ -344,6 +369,7 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
         lds_barrier();
         flush(PPT - 1, all_prev);
     }
+    step_prio<3>();
 }
 
 // One tile of the poll-mode kernel, step by step: loads, then tile_steps_v.
@@ -352,8 +378,9 @@ __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &
                                            int tid, int lane, int wave, bool sys = false)
 {
     u32x4 v[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3];
+    step_prio<0>();
     steps_load<PPT, 0, (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT)>(B, j, lane, wave, v, sys);
-    tile_steps_v<FW, LPM, PPT, WT>(p, lc, B, j, tid, lane, wave, v);
+    tile_steps_v<FW, LPM, PPT, WT>(p, lc, B, j, tid, lane, wave, v, sys);
 }
 
 // One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,
@@ -388,13 +415,13 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
         constexpr int W = COPK_STREAM_W < PPT ? COPK_STREAM_W : PPT;
         u32x4 v[W][3];
 #pragma unroll
-        for (int k = 0; k < W; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k]);
+        for (int k = 0; k < W; k++) load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k], sys);
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
             gather_step(sg, v[k % W], w3[k], w6[k], w7[k], w8[k]);
             if (k + W < PPT) {
                 __builtin_amdgcn_sched_barrier(0);
-                load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W]);
+                load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W], sys);
             }
         }
 #else

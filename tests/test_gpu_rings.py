@@ -233,6 +233,50 @@ def test_slots_rewritten_between_batches(gpu_ctx_factory, flags):
         assert m.info()["launches"] == 1   # served by one launch: no relaunch invalidated the caches
 
 
+@pytest.mark.parametrize("flags", [0, cg.PMD_DYNAMIC_TILES])
+def test_host_slots_rewritten_in_place(gpu_ctx_factory, flags):
+    """Slots in pinned host memory (cop_host_alloc_pinned: not coherent, so
+    a GPU L2 may keep a copy of a line it read) rewritten in place by the
+    CPU between batches, as the reference's fast path refills its rx ring
+    (switch.c:463-470). Every step of every 1024-packet tile must read the
+    new packets: the first step's loads and the later steps' refills alike
+    (a one-step load window refills three of four). Eight generations
+    through two 64k-packet slots, static and dynamic tiles."""
+    import ctypes
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    fw, _ = oracle_tables(rules)
+    B, P = 65536, 2
+    L_ = cg.lib()
+    hp = ctypes.c_void_p()
+    assert L_.cop_host_alloc_pinned(ctx.handle, B * P * 64, ctypes.byref(hp)) == 0
+    try:
+        gens = [np.ascontiguousarray(cg.gen_trace(0x5EED7600 + g, B, rules)) for g in range(8)]
+        for s_ in range(P):
+            ctypes.memmove(hp.value + s_ * B * 64, gens[s_].ctypes.data, B * 64)
+        dr = ctx.alloc(B * P * 8)
+        df = ctx.alloc(B * P * 4)
+        dc = ctx.alloc(P * nseg(B) * 4)
+        ring = cg.make_ring(hp.value, P, B, dr, B * 64, fwd_idx=df, fwd_slot=B, fwd_count=dc)
+        with ctx.pmd_start(ring, flags) as m:
+            for g in range(8):
+                s_ = g % P
+                if g >= P:
+                    ctypes.memmove(hp.value + s_ * B * 64, gens[g].ctypes.data, B * 64)
+                m.post(1)
+                m.wait()
+                res = dr.download(cg.RESULT_DT, B * P)[s_ * B:(s_ + 1) * B]
+                fwd = df.download(np.uint32, B * P)[s_ * B:(s_ + 1) * B]
+                cnt = dc.download(np.uint32, P * nseg(B))[s_ * nseg(B):(s_ + 1) * nseg(B)]
+                ro, fo = oracle_batch(gens[g], B, S | F, fw)
+                assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"generation {g}"
+                assert np.array_equal(seg_to_dense(fwd, cnt, B), fo), f"generation {g} list"
+            assert m.info()["launches"] == 1
+    finally:
+        L_.cop_host_free_pinned(ctx.handle, hp)
+
+
 def test_static_slots_contradicts_acquire(gpu_ctx_factory):
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)

@@ -71,7 +71,8 @@ for s in "$@"; do
       grep -h '^{"metric"' "$out/n2_shared.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("n2", d["value"], "overlap", d["windows_overlap"], "union", d["value_union"], "skew", d["windows"]["start_skew_us_median"], "c5", {k: d["secondary"]["fw_lpm_1m"].get(k) for k in ("value", "windows_overlap", "rccl_init", "error")})' ;;
     win1)
       # a one-step load window (libcopgpu_win1.so, -DCOPK_PMD_WIN=1) against
-      # the default two-step window, alternating, then both tails
+      # the then-default two-step window, alternating, then both tails
+      # (profiles/r05/check8; one step has been the default since)
       i=0
       for lib in main win1 main win1 main win1; do
         i=$((i + 1))
@@ -82,6 +83,25 @@ for s in "$@"; do
       step 300 "$out/tail_main.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
       COP_LIB="$R/ghost-dataplane_amd/libcopgpu_win1.so" step 300 "$out/tail_win1.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
       grep -h "post->done\|slot on CU (w // 256)  [04]" "$out/tail_main.log" "$out/tail_win1.log" ;;
+    ab:*)
+      # an experiment build (ghost-dataplane_amd/libcopgpu_<name>.so) against
+      # the default build on the driver's command, alternating three pairs,
+      # then both tails of the 20-batch post (tools/pmd_tail.py)
+      x=${s#ab:}; i=0
+      for lib in main $x main $x main $x; do
+        i=$((i + 1))
+        L=""; [ "$lib" != main ] && L="$R/ghost-dataplane_amd/libcopgpu_$x.so"
+        COP_LIB=$L step 300 "$out/ab_${lib}_$i.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS
+        grep -h '^{"metric"' "$out/ab_${lib}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("ab", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "dyn steady", p.get("dynamic_tiles", {}).get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$lib"
+      done
+      step 300 "$out/tail_main.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
+      COP_LIB="$R/ghost-dataplane_amd/libcopgpu_$x.so" step 300 "$out/tail_$x.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
+      grep -h "post->done\|slot on CU (w // 256)  [04]" "$out/tail_main.log" "$out/tail_$x.log" ;;
+    e2e)
+      # the end-to-end host-memory path (mbuf pool -> pinned staging -> H2D ->
+      # pipeline -> D2H), 1..16 gather threads, first pass checked bit-exact
+      step 300 "$out/e2e.log" python3 -u "$R/tools/e2e.py"
+      tail -8 "$out/e2e.log" ;;
     c5)
       step 300 "$out/c5_${C5_FORM:-dir}.log" $B --quick --workload fw_lpm_1m --steps 20 --warmup 5 --route-form "${C5_FORM:-dir}" $BENCH_ARGS
       line "$out/c5_${C5_FORM:-dir}.log" ;;
