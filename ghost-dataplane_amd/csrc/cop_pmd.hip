@@ -368,9 +368,11 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                     // (tests shorten the look-back's spin bound: the skipped
                     // tile's successors give up in well under a second)
                     const LookCtx lk{p.look, (uint32_t)(b + 1), &P.d_ctl[2], &P.d_ctl[0], P.test_skip ? 14u : 22u};
+                    body_prio<COPK_PMD_WT != 0, 0>();
                     ok = tile_body<FW, LPM, LAY, PPT, EXT, COPK_PMD_WT != 0>(
                         p, o, lc, pmd_batch(p, rg, slot, n, ntiles), (rs0 + slot) * tpb, j, lk, tid_i, lane_i, wave_i,
                         false, (size_t)(rs0 + slot) * tpb + j, sysld);
+                    body_prio<COPK_PMD_WT != 0, 3>();
                 }
             }
             if (stamp && tid == 0) st_stamp(&stamp[2], __builtin_amdgcn_s_memrealtime());   // tile body done

@@ -219,16 +219,32 @@ constexpr bool steps_ok()
 #ifndef COPK_PMD_WIN
 #define COPK_PMD_WIN 1
 #endif
-// experiment builds: wave priority by progress (s_setprio 3 for a tile's
-// first step down to 0 for its last and while waiting), so a CU's lagging
-// waves issue before the ones a step ahead
+// Wave priority by progress: s_setprio 3 for a tile's first step down to 0
+// for its last step and while the worker waits. A SIMD issues from the
+// highest-priority ready wave, then the oldest, so without it the CU's
+// oldest workers issue (and get their data) first and its youngest worker
+// finishes last. With it a wave that is a step behind issues first. The
+// driver's 20-batch post: 53.8 / 53.7 / 52.8 against 50.7 / 51.5 / 51.1
+// Gpkt/s, poll-mode steady state 0.59-0.61 against 0.56-0.57, the spread
+// between a CU's first and fifth worker 2.0 against 3.3 us
+// (profiles/r05/check10/, three alternating pairs on one box)
 #ifndef COPK_PMD_PRIO
-#define COPK_PMD_PRIO 0
+#define COPK_PMD_PRIO 1
 #endif
 template <int K>
 __device__ __forceinline__ void step_prio()
 {
     if constexpr (COPK_PMD_PRIO) __builtin_amdgcn_s_setprio(K >= 3 ? 0 : 3 - K);
+}
+// experiment builds: the same for the poll-mode tile body (global-probe
+// lookups), by phase: headers, lookups, outputs
+#ifndef COPK_PMD_PRIO_BODY
+#define COPK_PMD_PRIO_BODY 0
+#endif
+template <bool WT, int K>
+__device__ __forceinline__ void body_prio()
+{
+    if constexpr (WT && COPK_PMD_PRIO_BODY) step_prio<K>();
 }
 // the step's forward-list segment through LDS and out as 16-byte stores
 #ifndef COPK_PMD_STAGE_LIST
@@ -286,7 +302,8 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
     for (int k = 0; k < PPT; k++) {
         uint32_t w3[1], w6[1], w7[1], w8[1];
         if (COPK_PMD_PRIO) {
-            if (k == 1) step_prio<1>();
+            if (k == 0) step_prio<0>();   // (a prefetched tile starts at the waiting priority)
+            else if (k == 1) step_prio<1>();
             else if (k == 2) step_prio<2>();
             else if (k == 3) step_prio<3>();
         }
@@ -479,6 +496,7 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
 #pragma unroll
     for (int k = 0; k < PPT; k++) valid[k] = base + k * BLOCK + tid < B.n;
     if (sync_tables) __syncthreads();   // LDS-DMA table staging has landed
+    body_prio<WT, 1>();
 
     // ---- pass 1 (parse, route, LDS searches, tbl24 loads issued) ----
     uint32_t verdict[PPT], port[PPT], flags[PPT], rnh[PPT], fwe[PPT], lpe[PPT], lpe2[PPT], fwe2[PPT], src[PPT], dst[PPT];
@@ -494,6 +512,7 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
     // ---- pass 2 (tbl8 step) and the verdicts ----
     Counts cn;
     pass2<FW, LPM, PPT>(p, w3, src, dst, valid, fwe, lpe, lpe2, fwe2, verdict, flags, rnh, cn.total, cn.notv4);
+    body_prio<WT, 2>();
     const bool bins = EXT && FW != COPK_TBL_OFF && p.hit_region != nullptr;
     // segmented lists with no optional feature: the lean epilogue (counters
     // from ballots, folded into the list's barriers)
