@@ -970,7 +970,7 @@ def dry_run(args, rank, world, local, W, secondaries):
         runs, own, reduced, windows = [], [], [], []
         for r in range(max(1, args.repeats)):
             group.barrier()
-            t = 40e-3 * (1.0 + 0.01 * rank)   # rank r "takes" 40 (1 + r/100) ms per run
+            t = 80e-3 * (1.0 + 0.01 * rank)   # rank r "takes" 80 (1 + r/100) ms per run
             t0 = gate.open()
             time.sleep(t)
             t1 = copdist.monotonic_ns()

@@ -33,12 +33,12 @@ def test_spawn_two_ranks_one_line():
     ranks = j["config"]["ranks"]
     assert [x["rank"] for x in ranks] == [0, 1]
     assert sorted(x["device"] for x in ranks) == [0, 1]          # one device per rank
-    # max over ranks: rank 1 "takes" 40.4 ms, so the job rate is 2 x its rate
+    # max over ranks: rank 1 "takes" 80.8 ms, so the job rate is 2 x its rate
     b = 65536
-    assert abs(j["value"] - 2 * 20 * b / 40.4e-3 / 1e6) < 1e-3 * j["value"]
+    assert abs(j["value"] - 2 * 20 * b / 80.8e-3 / 1e6) < 1e-3 * j["value"]
     # the start gate opened both windows together
     assert j["windows"]["start_gate"] == "shm" and j["windows_overlap"] >= 0.9
-    assert 0 < j["value_union"] <= 2 * 20 * b / 40e-3 / 1e6 * 1.001
+    assert 0 < j["value_union"] <= 2 * 20 * b / 80e-3 / 1e6 * 1.001
     assert ranks[0]["mpkt_s"] > ranks[1]["mpkt_s"]
     # the CPU baseline rides every N's line (N > 1 lines had none)
     cb = j["cpu_baseline"]
@@ -115,10 +115,10 @@ def test_eight_ranks_gate_overlap_and_config5_block():
     assert j["windows_overlap"] >= 0.9, j["windows"]
     assert len(j["windows"]["per_run"]["overlap"]) == 5
     b = 65536
-    # value: max over ranks (rank 7 takes 42.8 ms); union: never above every
+    # value: max over ranks (rank 7 takes 85.6 ms); union: never above every
     # rank running its packets in the fastest rank's time
-    assert abs(j["value"] - 8 * 20 * b / 42.8e-3 / 1e6) < 1e-3 * j["value"]
-    assert j["value_union"] <= 8 * 20 * b / 40e-3 / 1e6 * 1.001
+    assert abs(j["value"] - 8 * 20 * b / 85.6e-3 / 1e6) < 1e-3 * j["value"]
+    assert j["value_union"] <= 8 * 20 * b / 80e-3 / 1e6 * 1.001
     c5 = j["secondary"]["fw_lpm_1m"]
     assert c5["rule_counters"] and c5["rccl_init"] == ["ok"] * 8
     B = 262144
