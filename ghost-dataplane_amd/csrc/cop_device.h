@@ -618,6 +618,36 @@ __device__ __forceinline__ void tbl8_step(const uint32_t *tbl8, uint32_t packed,
     }
 }
 
+// tbl8_step in two halves for one packet per lane, so a step pipeline can
+// issue a step's tbl8 load and use it one step later (tile_steps_v):
+// tbl8_issue loads the group entry (plain) or the run block's header word
+// (packed); tbl8_finish returns the entry (packed: the run's entry, one more
+// dependent load).
+struct T8 {
+    bool ext;
+    unsigned long long h;
+};
+__device__ __forceinline__ T8 tbl8_issue(const uint32_t *tbl8, uint32_t packed, uint32_t ip, uint32_t e)
+{
+    T8 t;
+    t.ext = (e & 0x03000000u) == 0x03000000u;
+    t.h = 0;
+    if (t.ext) {
+        if (!packed) t.h = tbl8[((size_t)(e & 0x00FFFFFFu) << 8) | (ip & 0xFFu)];
+        else t.h = ((const unsigned long long *)(tbl8 + ((size_t)(e & 0x00FFFFFFu) << 4)))[(ip & 0xFFu) >> 5];
+    }
+    return t;
+}
+__device__ __forceinline__ uint32_t tbl8_finish(const uint32_t *tbl8, uint32_t packed, uint32_t ip, uint32_t e,
+                                                const T8 &t)
+{
+    if (!t.ext) return e;
+    if (!packed) return (uint32_t)t.h;
+    const uint32_t bit = ip & 31u;
+    const uint32_t rank = (uint32_t)(t.h >> 32) + (uint32_t)__popc((uint32_t)t.h & (0xFFFFFFFFu >> (31u - bit)));
+    return tbl8[((size_t)(e & 0x00FFFFFFu) << 4) + 16u + rank - 1u];
+}
+
 // The bucketed route form's second round (COPK_TBL_BKT, lpm_bkt.c): for
 // each reached packet with candidates k0..k1 (start k0 <= ip, R(ip) <= k1),
 // one 64-byte read of pairs k0 .. k0 + 7 (four 16-byte loads, all PPT
@@ -686,7 +716,9 @@ __device__ __forceinline__ void bkt_step(const uint32_t *pairs, const uint32_t (
 // verdicts of stage FW (firewall.c:183-210) and stage LPM. Packets that did
 // not reach the coprocessor (stage P drop) keep their verdict. Counts the
 // FW stage's pkt_total / pkt_not_ipv4 (firewall.h:56-61) over valid packets.
-template <int FW, int LPM, int PPT>
+// LPM_T8 false: the route's tbl8 step was done by the caller (tbl8_issue /
+// tbl8_finish).
+template <int FW, int LPM, int PPT, bool LPM_T8 = true>
 __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[PPT], const uint32_t (&src)[PPT],
                                       const uint32_t (&dst)[PPT], const bool (&valid)[PPT], uint32_t (&fwe)[PPT],
                                       uint32_t (&lpe)[PPT], const uint32_t (&lpe2)[PPT], const uint32_t (&fwe2)[PPT],
@@ -702,7 +734,7 @@ __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[
     }
     if (FW == COPK_TBL_DIR) tbl8_step<PPT>(p.fw_tbl8, p.fw_tbl8_packed, src, fwe);
     if (FW == COPK_TBL_BKT) bkt_step<PPT>(p.fw_bpairs, src, fwe, fwe2, reached);
-    if (LPM == COPK_TBL_DIR) tbl8_step<PPT>(p.lpm_tbl8, p.lpm_tbl8_packed, dst, lpe);
+    if (LPM == COPK_TBL_DIR && LPM_T8) tbl8_step<PPT>(p.lpm_tbl8, p.lpm_tbl8_packed, dst, lpe);
     if (LPM == COPK_TBL_TRIE) trie_walk<PPT>(p.lpm_tnodes, p.lpm_tleaves, dst, lpe, reached);
     if (LPM == COPK_TBL_BKT) bkt_step<PPT>(p.lpm_bpairs, dst, lpe, lpe2, reached);
 #pragma unroll

@@ -63,10 +63,19 @@ __device__ __forceinline__ unsigned long long ld_u64(const unsigned long long *p
 }
 
 // Publish posted count h through a ring's gate (doorbell leaders, before they
-// raise the ring's relays): false once an exit has closed it.
-__device__ __forceinline__ bool gate_publish(unsigned long long *gate, unsigned long long h)
+// raise the ring's relays): false once an exit has closed it. guess: the
+// relay value the leader read in the same poll, usually the gate's value
+// (relays copy the gate), so the first compare-exchange goes out without a
+// load of the gate before it: one agent-scope round trip less between the
+// doorbell and the relays (profiles/r05/check12/tail_*.log: relay -> seen
+// 1.79 against 2.01 us, host post -> done 25.6 against 26.5 us). A wrong
+// guess costs what the load did: the failed exchange returns the gate.
+#ifndef COPK_PMD_GATE_GUESS
+#define COPK_PMD_GATE_GUESS 1
+#endif
+__device__ __forceinline__ bool gate_publish(unsigned long long *gate, unsigned long long h, unsigned long long guess)
 {
-    unsigned long long g = ld_u64(gate);
+    unsigned long long g = COPK_PMD_GATE_GUESS ? guess : ld_u64(gate);
     for (;;) {
         if (g >> COPK_PMD_GATE_SHIFT) return false;
         if ((g & GATE_POSTED) >= h) return true;   // another leader published as much
@@ -141,7 +150,7 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
         }
         if (leader) {
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-            if (h > hp && (COPK_PMD_NOGATE || gate_publish(gate, h))) {
+            if (h > hp && (COPK_PMD_NOGATE || gate_publish(gate, h, hp))) {
                 for (int x = 0; x < COPK_PMD_RELAYS; x++) atomicMax(relays + x * 16, h);
                 if (P.stamps && r == 0) {   // diagnostic: when each doorbell value was relayed
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2], h);
@@ -352,9 +361,13 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             const int wave_i = __builtin_amdgcn_readfirstlane(tid_i >> 6);
             bool ok = true;
             if constexpr (STEPS) {
-                if (j < ntiles)   // (a tile past a short batch's packets has nothing to do)
-                    tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0>(p, lc, pmd_batch(p, rg, slot, n, ntiles), j, tid_i,
-                                                                lane_i, wave_i, sysld);
+                // (a tile past a short batch's packets has nothing to do;
+                // the load form is picked per tile: cop_tile.h steps_load)
+                if (j < ntiles) {
+                    const CopKBatch bt = pmd_batch(p, rg, slot, n, ntiles);
+                    if (sysld) tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 1>(p, lc, bt, j, tid_i, lane_i, wave_i);
+                    else tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 0>(p, lc, bt, j, tid_i, lane_i, wave_i);
+                }
             } else {
                 if (P.test_skip && r == 0 && b == 0 && j + 1 == P.test_skip) {
                     ok = false;   // tests: this tile never runs nor publishes (its successors give up)
@@ -614,7 +627,10 @@ template <int FW>
 hipError_t pmd_lpm(const CopKPmd *p, int lpm, int lay, int ppt, int ext, uint32_t lds, hipStream_t s, int *occ)
 {
 #ifdef COPK_ISA_PROBE   // ISA inspection builds only: one instantiation (tools/isa.sh)
-    return pmd_one<FW, COPK_TBL_OFF, COPK_LAY_COALESCED, COPK_ISA_PROBE>(p, ext, lds, s, occ);
+#ifndef COPK_ISA_LPM
+#define COPK_ISA_LPM COPK_TBL_OFF
+#endif
+    return pmd_one<FW, COPK_ISA_LPM, COPK_LAY_COALESCED, COPK_ISA_PROBE>(p, ext, lds, s, occ);
 #else
     if constexpr (FW == COPK_TBL_BKT) {   // as cop_kernels.hip launch_lpm
         if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);

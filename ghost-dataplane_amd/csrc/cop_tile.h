@@ -183,13 +183,15 @@ __device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &
 }
 
 // Whether a tile can run step by step (tile_steps): segmented lists, no
-// optional feature, coalesced 64-byte slots, and LDS-only lookups (no
-// global probe whose latency a per-step pass 2 would serialise).
+// optional feature, coalesced 64-byte slots, the firewall in LDS, and the
+// route in LDS or DIR-24-8 (whose two dependent probes tile_steps_v
+// pipelines across steps; the trie's and the bucketed form's chains are
+// not).
 template <int FW, int LPM, int LAY, bool EXT>
 constexpr bool steps_ok()
 {
-    return !EXT && LAY == COPK_LAY_COALESCED && FW != COPK_TBL_DIR && FW != COPK_TBL_BKT && LPM != COPK_TBL_DIR &&
-           LPM != COPK_TBL_TRIE && LPM != COPK_TBL_BKT;
+    return !EXT && LAY == COPK_LAY_COALESCED && FW != COPK_TBL_DIR && FW != COPK_TBL_BKT && LPM != COPK_TBL_TRIE &&
+           LPM != COPK_TBL_BKT;
 }
 
 // One tile of the poll-mode kernel, step by step (tile_body does the same
@@ -252,10 +254,18 @@ __device__ __forceinline__ void body_prio()
 #endif
 // The header loads of steps K0 .. K1 - 1 of a tile (of tile_steps_v's
 // window: K1 <= W, all PPT steps when W == PPT): issued, not waited for.
-template <int PPT, int K0, int K1>
+// SYS: plain loads (0), system-coherent loads (1), or the run-time choice
+// sys_rt (2). A run-time choice between two load forms writing the same
+// registers makes the compiler's wait insertion put vmcnt waits before the
+// coherent form (for the other form's loads, on a path that never runs),
+// which wait for every store and probe still in flight; so the static order
+// picks 0 or 1 per tile (cop_pmd.hip). The dynamic order keeps 2: two
+// instantiations there hold more load registers than fit.
+template <int PPT, int K0, int K1, int SYS = 2>
 __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int lane, int wave,
-                                           u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], bool sys = false)
+                                           u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], bool sys_rt = false)
 {
+    const bool sys = SYS == 2 ? sys_rt : SYS == 1;
     static_assert(K1 <= (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT), "steps beyond the window");
     const StepGeom sg = step_geom(lane);
     const uint32_t base = j * (BLOCK * PPT);
@@ -265,14 +275,15 @@ __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int l
         load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k], sys);
 }
 
-// v: the tile's first W steps as steps_load issued them. sys: the later
+// v: the tile's first W steps as steps_load issued them. SYS: the later
 // steps' loads are system-coherent too (as steps_load's were: a reused or
 // host-memory slot, cop_pmd.hip)
-template <int FW, int LPM, int PPT, bool WT, bool STAGE_LIST = COPK_PMD_STAGE_LIST>
+template <int FW, int LPM, int PPT, bool WT, int SYS = 2, bool STAGE_LIST = COPK_PMD_STAGE_LIST>
 __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
                                              int tid, int lane, int wave,
-                                             u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], bool sys = false)
+                                             u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], bool sys_rt = false)
 {
+    const bool sys = SYS == 2 ? sys_rt : SYS == 1;
     static_assert(COPK_SEG == BLOCK, "one segment per tile step");
     const Tables &tb = lc.tb;
     constexpr int TILE = BLOCK * PPT;
@@ -298,30 +309,14 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
         if (lane < 16 && cc * 4u < len)
             st_list_chunk<WT>(&lc.cl.stage[k * BLOCK + cc * 4u], B.fwd_idx, pk + cc * 4u, B.n);
     };
-#pragma unroll
-    for (int k = 0; k < PPT; k++) {
-        uint32_t w3[1], w6[1], w7[1], w8[1];
-        if (COPK_PMD_PRIO) {
-            if (k == 0) step_prio<0>();   // (a prefetched tile starts at the waiting priority)
-            else if (k == 1) step_prio<1>();
-            else if (k == 2) step_prio<2>();
-            else if (k == 3) step_prio<3>();
-        }
-        gather_step(sg, v[k % W], w3[0], w6[0], w7[0], w8[0]);
-        if (k + W < PPT)
-            load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W], sys);
+    // step k's outputs once its verdicts are known: counts, records (lane
+    // i < 32 stores records 2i, 2i+1 of the wave's 64 packets as one 16-byte
+    // write-through store), the list segment and, after the last step, the
+    // counters
+    auto emit = [&](int k, bool valid0, uint32_t verdict0, uint32_t flags0, uint32_t port0, uint32_t rnh0) {
         const uint32_t pk0 = base + k * BLOCK;
-        const bool valid[1] = {pk0 + tid < B.n && B.n != 0};
-        uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1], ct = 0, cn = 0;
-        if (COPK_XP & 1) {
-            verdict[0] = (w3[0] ^ w6[0] ^ w7[0] ^ w8[0]) & 1u;
-            port[0] = w7[0] & 3u;
-            flags[0] = 0;
-            rnh[0] = w8[0];
-        } else {
-            pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2, fwe2);
-            pass2<FW, LPM, 1>(p, w3, src, dst, valid, fwe, lpe, lpe2, fwe2, verdict, flags, rnh, ct, cn);
-        }
+        const bool valid[1] = {valid0};
+        const uint32_t verdict[1] = {verdict0}, flags[1] = {flags0};
         const Counts c = wave_counts<FW, 1>(valid, verdict, flags);
         tot.total += c.total;
         tot.notv4 += c.notv4;
@@ -331,7 +326,7 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
         tot.noport += c.noport;
         tot.rhit += c.rhit;
         tot.rx += c.rx;
-        const unsigned long long bal = __ballot(valid[0] && verdict[0] == COPK_FORWARD);
+        const unsigned long long bal = __ballot(valid0 && verdict0 == COPK_FORWARD);
         if (lane == 0) {
             lc.cl.cnt[k * WAVES + wave] = (uint32_t)__popcll(bal);
             if (k == PPT - 1) {
@@ -341,11 +336,9 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
                 for (int q = 0; q < 8; q++) lc.s_red[wave * 8 + q] = c8[q];
             }
         }
-        // records of this step: lane i < 32 stores records 2i, 2i+1 of the
-        // wave's 64 packets as one 16-byte write-through store
-        const uint32_t rx = verdict[0] | (flags[0] << 8) | (port[0] << 16);
-        const uint32_t a0 = (uint32_t)__shfl((int)rx, 2 * i2), a1 = (uint32_t)__shfl((int)rnh[0], 2 * i2);
-        const uint32_t a2 = (uint32_t)__shfl((int)rx, 2 * i2 + 1), a3 = (uint32_t)__shfl((int)rnh[0], 2 * i2 + 1);
+        const uint32_t rx = verdict0 | (flags0 << 8) | (port0 << 16);
+        const uint32_t a0 = (uint32_t)__shfl((int)rx, 2 * i2), a1 = (uint32_t)__shfl((int)rnh0, 2 * i2);
+        const uint32_t a2 = (uint32_t)__shfl((int)rx, 2 * i2 + 1), a3 = (uint32_t)__shfl((int)rnh0, 2 * i2 + 1);
         const uint32_t idx = pk0 + (uint32_t)wave * 64u + 2u * (uint32_t)i2;
         if (lane < 32 && !(COPK_XP & 2)) {
             if (idx + 1 < B.n) st_u32x4<WT>(u32x4{a0, a1, a2, a3}, r, 2 * (long)idx);
@@ -356,7 +349,7 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
                 lds_barrier();
                 counters_add(p, lc.s_red, tid);
             }
-            continue;
+            return;
         }
         lds_barrier();
         // the step's segment: this wave's forwarded packets after the lower
@@ -381,6 +374,78 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
         }
         if (B.fwd_count && tid == 0 && pk0 < B.n) st_u32<WT>(all, B.fwd_count + pk0 / COPK_SEG);
         if (k == PPT - 1) counters_add(p, lc.s_red, tid);
+    };
+    auto prio = [&](int k) {
+        if (COPK_PMD_PRIO) {
+            if (k == 0) step_prio<0>();   // (a prefetched tile starts at the waiting priority)
+            else if (k == 1) step_prio<1>();
+            else if (k == 2) step_prio<2>();
+            else if (k == 3) step_prio<3>();
+        }
+    };
+    if constexpr (LPM != COPK_TBL_DIR) {
+        // LDS-only lookups: each step classified as its headers land
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            uint32_t w3[1], w6[1], w7[1], w8[1];
+            prio(k);
+            gather_step(sg, v[k % W], w3[0], w6[0], w7[0], w8[0]);
+            if (k + W < PPT)
+                load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W], sys);
+            const bool valid[1] = {base + k * BLOCK + tid < B.n && B.n != 0};
+            uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1], ct = 0,
+                cn = 0;
+            if (COPK_XP & 1) {
+                verdict[0] = (w3[0] ^ w6[0] ^ w7[0] ^ w8[0]) & 1u;
+                port[0] = w7[0] & 3u;
+                flags[0] = 0;
+                rnh[0] = w8[0];
+            } else {
+                pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2, fwe2);
+                pass2<FW, LPM, 1>(p, w3, src, dst, valid, fwe, lpe, lpe2, fwe2, verdict, flags, rnh, ct, cn);
+            }
+            emit(k, valid[0], verdict[0], flags[0], port[0], rnh[0]);
+        }
+    } else {
+        // The route's DIR-24-8 probes: two dependent global loads per packet
+        // (tbl24, then tbl8 for an extended entry: most wave-steps have one).
+        // A three-step pipeline keeps them off the step's critical path: in
+        // round k, step k's headers are gathered and classified and its tbl24
+        // probe issued, step k - 1's tbl8 load is issued (its tbl24 entry has
+        // landed), and step k - 2 is finished and written out.
+        static_assert(FW != COPK_TBL_DIR && FW != COPK_TBL_BKT, "firewall lookups in LDS only");
+        struct St {
+            uint32_t w3, src, dst, verdict, port, fwe, lpe;
+            bool valid;
+            T8 t8;
+        };
+        St a{}, b{}, c{};
+#pragma unroll
+        for (int k = 0; k < PPT + 2; k++) {
+            if (k < PPT) {
+                uint32_t w3[1], w6[1], w7[1], w8[1];
+                prio(k);
+                gather_step(sg, v[k % W], w3[0], w6[0], w7[0], w8[0]);
+                if (k + W < PPT)
+                    load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W],
+                              sys);
+                uint32_t verdict[1], port[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1];
+                pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2, fwe2);
+                a = St{w3[0], src[0], dst[0], verdict[0], port[0], fwe[0], lpe[0],
+                       base + k * BLOCK + tid < B.n && B.n != 0, T8{false, 0ull}};
+            }
+            if (k >= 1 && k <= PPT) b.t8 = tbl8_issue(p.lpm_tbl8, p.lpm_tbl8_packed, b.dst, b.lpe);
+            if (k >= 2) {
+                const uint32_t w3[1] = {c.w3}, src[1] = {c.src}, dst[1] = {c.dst}, lpe2[1] = {0}, fwe2[1] = {0};
+                const bool valid[1] = {c.valid};
+                uint32_t verdict[1] = {c.verdict}, fwe[1] = {c.fwe}, flags[1], rnh[1], ct = 0, cn = 0;
+                uint32_t lpe[1] = {tbl8_finish(p.lpm_tbl8, p.lpm_tbl8_packed, c.dst, c.lpe, c.t8)};
+                pass2<FW, LPM, 1, false>(p, w3, src, dst, valid, fwe, lpe, lpe2, fwe2, verdict, flags, rnh, ct, cn);
+                emit(k - 2, valid[0], verdict[0], flags[0], c.port, rnh[0]);
+            }
+            c = b;
+            b = a;
+        }
     }
     if (staged) {
         lds_barrier();
@@ -390,14 +455,14 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
 }
 
 // One tile of the poll-mode kernel, step by step: loads, then tile_steps_v.
-template <int FW, int LPM, int PPT, bool WT>
+template <int FW, int LPM, int PPT, bool WT, int SYS>
 __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
-                                           int tid, int lane, int wave, bool sys = false)
+                                           int tid, int lane, int wave)
 {
     u32x4 v[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3];
     step_prio<0>();
-    steps_load<PPT, 0, (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT)>(B, j, lane, wave, v, sys);
-    tile_steps_v<FW, LPM, PPT, WT>(p, lc, B, j, tid, lane, wave, v, sys);
+    steps_load<PPT, 0, (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT), SYS>(B, j, lane, wave, v);
+    tile_steps_v<FW, LPM, PPT, WT, SYS>(p, lc, B, j, tid, lane, wave, v);
 }
 
 // One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,

@@ -101,9 +101,11 @@ for s in "$@"; do
       # the poll-mode FW + LPM 100k post with step-by-step tiles (the route's
       # DIR-24-8 probes pipelined across steps) against whole-tile bodies
       # ($COP_PMD_STEPWISE=0), alternating, at the driver's 20 steps
+      i=0
       for v in 0 1 0 1 0 1; do
-        COP_PMD_STEPWISE=$v step 300 "$out/steps_fwlpm_$v.log" $B --workload fw_lpm --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS
-        grep -h '^{"metric"' "$out/steps_fwlpm_$v.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("stepwise", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$v"
+        i=$((i + 1))
+        COP_PMD_STEPWISE=$v step 300 "$out/steps_fwlpm_${v}_$i.log" $B --workload fw_lpm --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS
+        grep -h '^{"metric"' "$out/steps_fwlpm_${v}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("stepwise", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$v"
       done ;;
     e2e)
       # the end-to-end host-memory path (mbuf pool -> pinned staging -> H2D ->
