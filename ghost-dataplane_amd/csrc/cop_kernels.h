@@ -204,7 +204,8 @@ struct CopKPmd {
     // are claimed from a ticket counter, tile T = seq0r[r] * tiles per batch
     // + the T-th claim, instead of the static T = w + k * workers; a worker
     // claims its next tile and issues that tile's header loads before it
-    // finishes the current one ($COP_PMD_DYN)
+    // finishes the current one ($COP_PMD_DYN); 2: the same prefetch in the
+    // static order, no tickets ($COP_PMD_PF)
     uint32_t dyn;
     uint32_t tk_lanes;                   // ticket lanes per ring (1, or 8: one per XCD-sized worker group)
     unsigned long long *d_ticket;        // device: ring r's lane x claim counter at [16 (r * COPK_PMD_TK_LANES + x)]

@@ -435,7 +435,10 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             // x owning tiles j = x, x + nx, ... of every batch, so no one
             // counter takes every claim (one counter for all 1536 workers
             // held a 256-packet-tile kernel at ~80 claims per us)
-            const uint32_t nx = (P.tk_lanes > 1 && tpb % P.tk_lanes == 0) ? P.tk_lanes : 1u;
+            // P.dyn 2: the static order (T = wr, wr + G, ...: no tickets)
+            // with the same next-tile prefetch
+            const bool det = P.dyn == 2u;
+            const uint32_t nx = (!det && P.tk_lanes > 1 && tpb % P.tk_lanes == 0) ? P.tk_lanes : 1u;
             const uint32_t xl = wr % nx;
             const uint32_t per = tpb / nx;   // tiles of one batch in one lane
             unsigned long long *ticket = P.d_ticket + ((size_t)r * COPK_PMD_TK_LANES + xl) * 16;
@@ -454,7 +457,9 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                                        __HIP_MEMORY_SCOPE_SYSTEM);
                 pend = false;
             };
-            auto claim = [&] { return __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+            auto claim = [&](unsigned long long cur) {
+                return det ? cur + G : __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
             auto tk_get = [&] { return ((unsigned long long)s_tk[1] << 32) | s_tk[0]; };
             // the first claim. A worker holds one unserved ticket while it
             // waits for a post and claims its next tile only once the
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             // (1024-packet tiles: 29 against 46 Gpkt/s at 20 steps,
             // profiles/r05/check5/)
             if (tid == 0) {
-                const unsigned long long t0 = claim();
+                const unsigned long long t0 = det ? (unsigned long long)wr : claim(0);
                 s_tk[0] = (uint32_t)t0;
                 s_tk[1] = (uint32_t)(t0 >> 32);
             }
@@ -530,7 +535,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                 // T is posted: claim the next tile (its return lands after
                 // T's loads, which this tile waits for anyway)
                 if (tid == 0) {
-                    const unsigned long long tn = claim();
+                    const unsigned long long tn = claim(T);
                     s_tk[0] = (uint32_t)tn;
                     s_tk[1] = (uint32_t)(tn >> 32);
                 }

@@ -2031,6 +2031,7 @@ struct cop_pmd {
     uint32_t n_rings = 1, n_slots = 0, tpb = 0, per_cu = 0, ring_n = 0;
     uint32_t acquire = 4;       // CopKPmd::sys_acquire: 4 coherent loads on slot reuse (default), 3 on every tile, 0 never
     bool dyn = false;           // CopKPmd::dyn: dynamic tiles
+    bool pf = false;            // CopKPmd::dyn 2: the static order with the next tile prefetched
     std::atomic<uint32_t> launches{0};
     uint32_t pauses = 0;                    // pmd_pause calls that stopped a running kernel
     bool was_live = false;                  // pmd_pause found it running (pmd_resume relaunches)
@@ -2196,7 +2197,7 @@ static void pmd_size(cop_pmd *m)
     if (const char *e = getenv("COP_PMD_RELAY_STRIDE")) m->P.relay_stride = std::max(1u, (uint32_t)atoi(e));
     m->P.poll_backoff = 3;
     m->P.stepwise = getenv("COP_PMD_STEPWISE") && !atoi(getenv("COP_PMD_STEPWISE")) ? 0u : 1u;
-    m->P.dyn = m->dyn ? 1u : 0u;
+    m->P.dyn = m->dyn ? 1u : m->pf ? 2u : 0u;
     // ticket lanes of dynamic tiles: 8 unless $COP_PMD_TK_LANES says 1
     m->P.tk_lanes = COPK_PMD_TK_LANES;
     if (const char *e = getenv("COP_PMD_TK_LANES")) m->P.tk_lanes = atoi(e) == 1 ? 1u : (uint32_t)COPK_PMD_TK_LANES;
@@ -2411,6 +2412,9 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
     const char *dyn_env = getenv("COP_PMD_DYN");
     m->dyn = seg && (dyn_env ? atoi(dyn_env) != 0 : (flags & COP_PMD_DYNAMIC_TILES) != 0);
     if (m->dyn && dyn_env && atoi(dyn_env) == 1) ppt = 1;
+    // A/B runs: $COP_PMD_PF=1 the static order with the next tile's first
+    // step prefetched during the current one (segmented lists)
+    m->pf = seg && !m->dyn && getenv("COP_PMD_PF") && atoi(getenv("COP_PMD_PF")) != 0;
     if (c->ppt_override) ppt = c->ppt_override;
     pl.ppt = ppt;
     m->ppt = ppt;

@@ -97,6 +97,22 @@ for s in "$@"; do
       step 300 "$out/tail_main.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
       COP_LIB="$R/ghost-dataplane_amd/libcopgpu_$x.so" step 300 "$out/tail_$x.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
       grep -h "post->done\|slot on CU (w // 256)  [04]" "$out/tail_main.log" "$out/tail_$x.log" ;;
+    envab:*)
+      # an environment setting (envab:NAME=VALUE) against the default on the
+      # driver's command, alternating three pairs, then the poll-mode,
+      # segmented and ring GPU tests with it set
+      kv=${s#envab:}; i=0
+      for v in off on off on off on; do
+        i=$((i + 1))
+        if [ $v = on ]; then
+          env "$kv" "$R/tools/gpu_step.sh" 300 "$out/env_${v}_$i.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS || exit 99
+        else
+          step 300 "$out/env_${v}_$i.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS
+        fi
+        grep -h '^{"metric"' "$out/env_${v}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("env", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "dyn steady", p.get("dynamic_tiles", {}).get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$v"
+      done
+      env "$kv" "$R/tools/gpu_step.sh" 600 "$out/pytest_env.log" python3 -u -m pytest "$R/tests" -m gpu -v -k "pmd or seg or rings or rewritten" --timeout 120 --timeout-method thread || exit 99
+      grep -E "FAILED|ERROR|passed|failed" "$out/pytest_env.log" | tail -4 ;;
     steps_ab)
       # the poll-mode FW + LPM 100k post with step-by-step tiles (the route's
       # DIR-24-8 probes pipelined across steps) against whole-tile bodies
