@@ -473,6 +473,9 @@ def measure(args, name, rank, world, dev, group, gate, primary):
                 pmd.run(n_long)
                 d_longs.append(time.perf_counter() - t0)
             for _ in range(11):
+                # as the line's runs: a barrier between posts (back to back,
+                # the next post met workers still counting the last one)
+                group.barrier()
                 t0 = time.perf_counter()
                 pmd.run(args.steps)
                 d_short.append(time.perf_counter() - t0)
@@ -481,7 +484,7 @@ def measure(args, name, rank, world, dev, group, gate, primary):
             dyn = {"workers": di["workers"], "packets_per_tile": di["packets_per_tile"],
                    "steady_mpkt_s": round(n_long * B / dl / 1e6, 3), "steady_ms": round(dl * 1e3, 4),
                    f"mpkt_s_{args.steps}_steps": round(args.steps * B / float(np.median(d_short)) / 1e6, 3),
-                   "note": "not the line's value: host-timed posts of this kernel, no gate"}
+                   "note": "not the line's value: host-timed posts of this kernel, a barrier between them, no gate"}
         res["pmd_info"] = {"workers": info["workers"], "workers_per_cu": info["workers_per_cu"],
                            "packets_per_tile": info["packets_per_tile"], "launches": info["launches"],
                            "steady_batches": n_long, "steady_mpkt_s": round(n_long * B / t_long / 1e6, 3),
