@@ -221,6 +221,11 @@ constexpr bool steps_ok()
 #ifndef COPK_PMD_WIN
 #define COPK_PMD_WIN 1
 #endif
+template <int PPT, int WIN>
+constexpr int win_of()
+{
+    return WIN < PPT ? WIN : PPT;
+}
 // Wave priority by progress: s_setprio 3 for a tile's first step down to 0
 // for its last step and while the worker waits. A SIMD issues from the
 // highest-priority ready wave, then the oldest, so without it the CU's
@@ -261,12 +266,12 @@ __device__ __forceinline__ void body_prio()
 // which wait for every store and probe still in flight; so the static order
 // picks 0 or 1 per tile (cop_pmd.hip). The dynamic order keeps 2: two
 // instantiations there hold more load registers than fit.
-template <int PPT, int K0, int K1, int SYS = 2>
+template <int PPT, int K0, int K1, int SYS = 2, int WIN = COPK_PMD_WIN>
 __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int lane, int wave,
-                                           u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], bool sys_rt = false)
+                                           u32x4 (&v)[win_of<PPT, WIN>()][3], bool sys_rt = false)
 {
     const bool sys = SYS == 2 ? sys_rt : SYS == 1;
-    static_assert(K1 <= (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT), "steps beyond the window");
+    static_assert(K1 <= win_of<PPT, WIN>(), "steps beyond the window");
     const StepGeom sg = step_geom(lane);
     const uint32_t base = j * (BLOCK * PPT);
     const uint32_t last = B.n ? B.n - 1 : 0u;
@@ -278,10 +283,11 @@ __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int l
 // v: the tile's first W steps as steps_load issued them. SYS: the later
 // steps' loads are system-coherent too (as steps_load's were: a reused or
 // host-memory slot, cop_pmd.hip)
-template <int FW, int LPM, int PPT, bool WT, int SYS = 2, bool STAGE_LIST = COPK_PMD_STAGE_LIST>
+template <int FW, int LPM, int PPT, bool WT, int SYS = 2, int WIN = COPK_PMD_WIN,
+          bool STAGE_LIST = COPK_PMD_STAGE_LIST>
 __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
-                                             int tid, int lane, int wave,
-                                             u32x4 (&v)[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3], bool sys_rt = false)
+                                             int tid, int lane, int wave, u32x4 (&v)[win_of<PPT, WIN>()][3],
+                                             bool sys_rt = false)
 {
     const bool sys = SYS == 2 ? sys_rt : SYS == 1;
     static_assert(COPK_SEG == BLOCK, "one segment per tile step");
@@ -293,7 +299,7 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
     // a window of W steps in flight: step k + W is loaded once step k is
     // gathered, so the CU's queue holds every worker's early steps before
     // any worker's late ones and the workers' last steps land together
-    constexpr int W = COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT;
+    constexpr int W = win_of<PPT, WIN>();
     Counts tot;
     uint32_t *r = (uint32_t *)B.results;
     const int i2 = lane & 31;
@@ -455,14 +461,14 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
 }
 
 // One tile of the poll-mode kernel, step by step: loads, then tile_steps_v.
-template <int FW, int LPM, int PPT, bool WT, int SYS>
+template <int FW, int LPM, int PPT, bool WT, int SYS, int WIN = COPK_PMD_WIN>
 __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
                                            int tid, int lane, int wave)
 {
-    u32x4 v[COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT][3];
+    u32x4 v[win_of<PPT, WIN>()][3];
     step_prio<0>();
-    steps_load<PPT, 0, (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT), SYS>(B, j, lane, wave, v);
-    tile_steps_v<FW, LPM, PPT, WT, SYS>(p, lc, B, j, tid, lane, wave, v);
+    steps_load<PPT, 0, win_of<PPT, WIN>(), SYS, WIN>(B, j, lane, wave, v);
+    tile_steps_v<FW, LPM, PPT, WT, SYS, WIN>(p, lc, B, j, tid, lane, wave, v);
 }
 
 // One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,

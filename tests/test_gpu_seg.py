@@ -388,14 +388,17 @@ def test_pmd_idle_exit_counts_every_batch_once(gpu_ctx_factory, monkeypatch):
     assert np.array_equal(ctx.rule_counters(), want)
 
 
-@pytest.mark.parametrize("fw_dir", [False, True])
-def test_pmd_seg_fw_lpm_dir_probes(gpu_ctx_factory, fw_dir):
-    """The poll-mode kernel with segmented lists and DIR-24-8 stages (they
-    run in tile_body: a step-by-step form with the probes one step ahead
-    was bit-exact but slower): FW + LPM 100k with the
-    route stage in HBM, and with the firewall forced to DIR-24-8 too; a
-    post of every slot, then posts of 1, 5 and 12 batches that wrap the
-    6-slot ring."""
+@pytest.mark.parametrize("fw_dir,tbl8", [(False, "plain"), (False, "packed"), (True, "plain")])
+def test_pmd_seg_fw_lpm_dir_probes(gpu_ctx_factory, monkeypatch, fw_dir, tbl8):
+    """The poll-mode kernel with segmented lists and DIR-24-8 stages: FW +
+    LPM 100k with the route stage in HBM runs step by step, the route's
+    tbl24 and tbl8 probes pipelined across steps (cop_tile.h tile_steps_v;
+    DESIGN.md §15.9), with the tbl8 groups plain or as packed run blocks
+    (a second dependent load); with the firewall forced to DIR-24-8 too it
+    runs in tile_body. A post of every slot, then posts of 1, 5 and 12
+    batches that wrap the 6-slot ring (so later tiles take the coherent
+    load form)."""
+    monkeypatch.setenv("COP_TBL8", tbl8)
     rules = fw1k()
     rts = cg.gen_rules(0x5EED2004, 100000, cg.GEN_ROUTES, 0)
     ctx = gpu_ctx_factory(stages=S | F | L,

@@ -92,7 +92,7 @@ for s in "$@"; do
         i=$((i + 1))
         L=""; [ "$lib" != main ] && L="$R/ghost-dataplane_amd/libcopgpu_$x.so"
         COP_LIB=$L step 300 "$out/ab_${lib}_$i.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS
-        grep -h '^{"metric"' "$out/ab_${lib}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("ab", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "dyn steady", p.get("dynamic_tiles", {}).get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$lib"
+        grep -h '^{"metric"' "$out/ab_${lib}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); print("ab", sys.argv[1], d["value"], "timed", d["roofline"]["frac_timed"], "steady", p.get("steady_frac"), "dyn steady", p.get("dynamic_tiles", {}).get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"), "16 in flight", p.get("one_batch_posts", {}).get("mpkt_s"))' "$lib"
       done
       step 300 "$out/tail_main.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
       COP_LIB="$R/ghost-dataplane_amd/libcopgpu_$x.so" step 300 "$out/tail_$x.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
