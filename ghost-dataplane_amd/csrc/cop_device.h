@@ -161,6 +161,30 @@ __device__ __forceinline__ uint32_t ivt_search(const uint32_t *S, uint32_t m, ui
     return k;
 }
 
+// ivt_search's interval value V[k] directly: the last lift level reads the
+// candidate's start and both candidates' values together, so the value
+// costs no dependent LDS read of its own (1 + lv reads in the chain, not
+// 2 + lv). Experiment builds: COPK_IVT_VALUE.
+#ifndef COPK_IVT_VALUE
+#define COPK_IVT_VALUE 0
+#endif
+__device__ __forceinline__ uint32_t ivt_value(const uint32_t *S, const uint32_t *V, uint32_t m, uint32_t ib, uint32_t lv,
+                                              uint32_t ip)
+{
+    if (!COPK_IVT_VALUE || lv == 0) return V[ivt_search(S, m, ib, lv, ip)];
+    const uint16_t *idx = (const uint16_t *)(S + m);
+    const uint32_t b = ip >> (32u - ib);
+    uint32_t k = idx[b];
+    const uint32_t hi = idx[b + 1];
+    for (uint32_t step = (1u << lv) >> 1; step > 1; step >>= 1) {
+        const uint32_t c = min(k + step, hi);
+        if (S[c] <= ip) k = c;
+    }
+    const uint32_t c = min(k + 1, hi);
+    const uint32_t sc = S[c], vk = V[k], vc = V[c];
+    return sc <= ip ? vc : vk;
+}
+
 // Decoupled look-back over one chain of tile granules (tile t at
 // chain[t * stride]): publish this tile's aggregate, read up to 256
 // predecessors per round (four loads per lane: lane l reads tiles qhi-l,
@@ -520,10 +544,10 @@ __device__ __forceinline__ void pass1(const CopKParams &p, const Tables &t, cons
         // HBM probes only for packets that reach the coprocessor (masked-off
         // lanes send no request); the others keep their stage-P verdict
         const bool reach = verdict[k] == COPK_FORWARD;
-        if (FW == COPK_TBL_IVT) fwe[k] = t.fw_v[ivt_search(t.fw_s, p.fw_m, p.fw_ib, p.fw_lv, src[k])];
+        if (FW == COPK_TBL_IVT) fwe[k] = ivt_value(t.fw_s, t.fw_v, p.fw_m, p.fw_ib, p.fw_lv, src[k]);
         if (FW == COPK_TBL_DIR) fwe[k] = reach ? probe_ld(&p.fw_tbl24[src[k] >> 8], p.probe_nt) : 0u;
         if (FW == COPK_TBL_BKT) bkt_issue(p.fw_bidx, p.fw_ib, src[k], reach, fwe[k], fwe2[k]);
-        if (LPM == COPK_TBL_IVT) lpe[k] = t.lp_v[ivt_search(t.lp_s, p.lpm_m, p.lpm_ib, p.lpm_lv, dst[k])];
+        if (LPM == COPK_TBL_IVT) lpe[k] = ivt_value(t.lp_s, t.lp_v, p.lpm_m, p.lpm_ib, p.lpm_lv, dst[k]);
         if (LPM == COPK_TBL_DIR) lpe[k] = reach ? probe_ld(&p.lpm_tbl24[dst[k] >> 8], p.probe_nt) : 0u;
         if (LPM == COPK_TBL_TRIE) lpe[k] = t.lp_s[dst[k] >> 20];
         if (LPM == COPK_TBL_BKT) bkt_issue(p.lpm_bidx, p.lpm_ib, dst[k], reach, lpe[k], lpe2[k]);

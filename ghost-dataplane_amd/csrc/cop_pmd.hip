@@ -365,8 +365,9 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                 // the load form is picked per tile: cop_tile.h steps_load)
                 if (j < ntiles) {
                     const CopKBatch bt = pmd_batch(p, rg, slot, n, ntiles);
-                    if (sysld) tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 1>(p, lc, bt, j, tid_i, lane_i, wave_i);
-                    else tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 0>(p, lc, bt, j, tid_i, lane_i, wave_i);
+                    constexpr int WIN = LPM == COPK_TBL_DIR ? COPK_PMD_WIN_DIR : COPK_PMD_WIN;
+                    if (sysld) tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 1, WIN>(p, lc, bt, j, tid_i, lane_i, wave_i);
+                    else tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 0, WIN>(p, lc, bt, j, tid_i, lane_i, wave_i);
                 }
             } else {
                 if (P.test_skip && r == 0 && b == 0 && j + 1 == P.test_skip) {

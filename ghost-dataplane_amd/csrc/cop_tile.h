@@ -221,6 +221,10 @@ constexpr bool steps_ok()
 #ifndef COPK_PMD_WIN
 #define COPK_PMD_WIN 1
 #endif
+// experiment builds: the window of the route's DIR-24-8 step pipeline
+#ifndef COPK_PMD_WIN_DIR
+#define COPK_PMD_WIN_DIR COPK_PMD_WIN
+#endif
 template <int PPT, int WIN>
 constexpr int win_of()
 {
