@@ -164,9 +164,12 @@ __device__ __forceinline__ uint32_t ivt_search(const uint32_t *S, uint32_t m, ui
 // ivt_search's interval value V[k] directly: the last lift level reads the
 // candidate's start and both candidates' values together, so the value
 // costs no dependent LDS read of its own (1 + lv reads in the chain, not
-// 2 + lv). Experiment builds: COPK_IVT_VALUE.
+// 2 + lv). The driver's command 53,975 / 53,512 / 53,514 against 53,359 /
+// 51,514 / 52,191 Mpkt/s, three alternating pairs on one box
+// (profiles/r05/check21/); COPK_IVT_VALUE=0 reads the value after the
+// search.
 #ifndef COPK_IVT_VALUE
-#define COPK_IVT_VALUE 0
+#define COPK_IVT_VALUE 1
 #endif
 __device__ __forceinline__ uint32_t ivt_value(const uint32_t *S, const uint32_t *V, uint32_t m, uint32_t ib, uint32_t lv,
                                               uint32_t ip)
