@@ -261,6 +261,22 @@ __device__ __forceinline__ void body_prio()
 #ifndef COPK_PMD_STAGE_LIST
 #define COPK_PMD_STAGE_LIST 1
 #endif
+// Experiment builds (COPK_SEG_WAVE, 1024-packet tiles): wave w of a tile
+// owns its segment w (packets w*256 .. w*256+255 of the tile) and walks it in
+// four steps of 64 packets, so a segment's list is one wave's forwarded
+// packets in order and no step needs a barrier; by default step k of a tile
+// is its segment k, 64 packets per wave, with a barrier per step.
+#ifndef COPK_SEG_WAVE
+#define COPK_SEG_WAVE 0
+#endif
+// the first packet of wave `wave`'s 64 packets in step k, from the tile's base
+template <int PPT>
+__device__ __forceinline__ uint32_t step_off(int k, int wave)
+{
+    if constexpr (COPK_SEG_WAVE && PPT == WAVES) return (uint32_t)(wave * PPT * 64 + k * 64);
+    else return (uint32_t)(k * BLOCK + wave * 64);
+}
+
 // The header loads of steps K0 .. K1 - 1 of a tile (of tile_steps_v's
 // window: K1 <= W, all PPT steps when W == PPT): issued, not waited for.
 // SYS: plain loads (0), system-coherent loads (1), or the run-time choice
@@ -281,7 +297,7 @@ __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int l
     const uint32_t last = B.n ? B.n - 1 : 0u;
 #pragma unroll
     for (int k = K0; k < K1; k++)
-        load_step(sg, B.pkts + B.data_off, B.stride, base + k * BLOCK + wave * 64, last, v[k], sys);
+        load_step(sg, B.pkts + B.data_off, B.stride, base + step_off<PPT>(k, wave), last, v[k], sys);
 }
 
 // v: the tile's first W steps as steps_load issued them. SYS: the later
@@ -323,8 +339,10 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
     // i < 32 stores records 2i, 2i+1 of the wave's 64 packets as one 16-byte
     // write-through store), the list segment and, after the last step, the
     // counters
+    uint32_t run = 0;   // COPK_SEG_WAVE: the wave's segment list so far
     auto emit = [&](int k, bool valid0, uint32_t verdict0, uint32_t flags0, uint32_t port0, uint32_t rnh0) {
         const uint32_t pk0 = base + k * BLOCK;
+        const uint32_t wb = base + step_off<PPT>(k, wave);   // this wave's 64 packets
         const bool valid[1] = {valid0};
         const uint32_t verdict[1] = {verdict0}, flags[1] = {flags0};
         const Counts c = wave_counts<FW, 1>(valid, verdict, flags);
@@ -349,7 +367,7 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
         const uint32_t rx = verdict0 | (flags0 << 8) | (port0 << 16);
         const uint32_t a0 = (uint32_t)__shfl((int)rx, 2 * i2), a1 = (uint32_t)__shfl((int)rnh0, 2 * i2);
         const uint32_t a2 = (uint32_t)__shfl((int)rx, 2 * i2 + 1), a3 = (uint32_t)__shfl((int)rnh0, 2 * i2 + 1);
-        const uint32_t idx = pk0 + (uint32_t)wave * 64u + 2u * (uint32_t)i2;
+        const uint32_t idx = wb + 2u * (uint32_t)i2;
         if (lane < 32 && !(COPK_XP & 2)) {
             if (idx + 1 < B.n) st_u32x4<WT>(u32x4{a0, a1, a2, a3}, r, 2 * (long)idx);
             else if (idx < B.n) st_u32x2<WT>(u32x2{a0, a1}, (u32x2 *)&r[2 * (size_t)idx]);
@@ -357,6 +375,33 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
         if (COPK_XP & 4) {
             if (k == PPT - 1) {
                 lds_barrier();
+                counters_add(p, lc.s_red, tid);
+            }
+            return;
+        }
+        if constexpr (COPK_SEG_WAVE && PPT == WAVES) {
+            // segment w = this wave's: its list is the wave's own forwarded
+            // packets in order (no other wave's counts needed)
+            const uint32_t sb = base + (uint32_t)wave * COPK_SEG;
+            const uint32_t rank = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            if (staged) {
+                if ((bal >> lane) & 1ull) lc.cl.stage[wave * COPK_SEG + rank] = wb + (uint32_t)lane;
+            } else if (B.fwd_idx && ((bal >> lane) & 1ull)) {
+                st_u32<WT>(wb + (uint32_t)lane, &B.fwd_idx[sb + rank]);
+            }
+            run += (uint32_t)__popcll(bal);
+            if (k == PPT - 1) {
+                if (staged) {
+                    // read back by the wave's other lanes: LDS operations of one
+                    // wave complete in order; keep the compiler from moving them
+                    asm volatile("" ::: "memory");
+                    if ((uint32_t)lane * 4u < run)
+                        st_list_chunk<WT>(&lc.cl.stage[wave * COPK_SEG + lane * 4], B.fwd_idx, sb + (uint32_t)lane * 4u,
+                                          B.n);
+                }
+                if (B.fwd_count && lane == 0 && sb < B.n) st_u32<WT>(run, B.fwd_count + sb / COPK_SEG);
+                lds_barrier();   // every wave's counters in s_red
                 counters_add(p, lc.s_red, tid);
             }
             return;
@@ -401,8 +446,8 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
             prio(k);
             gather_step(sg, v[k % W], w3[0], w6[0], w7[0], w8[0]);
             if (k + W < PPT)
-                load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W], sys);
-            const bool valid[1] = {base + k * BLOCK + tid < B.n && B.n != 0};
+                load_step(sg, B.pkts + B.data_off, B.stride, base + step_off<PPT>(k + W, wave), last, v[k % W], sys);
+            const bool valid[1] = {base + step_off<PPT>(k, wave) + (uint32_t)lane < B.n && B.n != 0};
             uint32_t verdict[1], port[1], flags[1], rnh[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1], ct = 0,
                 cn = 0;
             if (COPK_XP & 1) {
@@ -437,12 +482,12 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
                 prio(k);
                 gather_step(sg, v[k % W], w3[0], w6[0], w7[0], w8[0]);
                 if (k + W < PPT)
-                    load_step(sg, B.pkts + B.data_off, B.stride, base + (k + W) * BLOCK + wave * 64, last, v[k % W],
+                    load_step(sg, B.pkts + B.data_off, B.stride, base + step_off<PPT>(k + W, wave), last, v[k % W],
                               sys);
                 uint32_t verdict[1], port[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1];
                 pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2, fwe2);
                 a = St{w3[0], src[0], dst[0], verdict[0], port[0], fwe[0], lpe[0],
-                       base + k * BLOCK + tid < B.n && B.n != 0, T8{false, 0ull}};
+                       base + step_off<PPT>(k, wave) + (uint32_t)lane < B.n && B.n != 0, T8{false, 0ull}};
             }
             if (k >= 1 && k <= PPT) b.t8 = tbl8_issue(p.lpm_tbl8, p.lpm_tbl8_packed, b.dst, b.lpe);
             if (k >= 2) {
@@ -457,7 +502,7 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
             b = a;
         }
     }
-    if (staged) {
+    if (staged && !(COPK_SEG_WAVE && PPT == WAVES)) {
         lds_barrier();
         flush(PPT - 1, all_prev);
     }
