@@ -261,13 +261,16 @@ __device__ __forceinline__ void body_prio()
 #ifndef COPK_PMD_STAGE_LIST
 #define COPK_PMD_STAGE_LIST 1
 #endif
-// Experiment builds (COPK_SEG_WAVE, 1024-packet tiles): wave w of a tile
-// owns its segment w (packets w*256 .. w*256+255 of the tile) and walks it in
-// four steps of 64 packets, so a segment's list is one wave's forwarded
-// packets in order and no step needs a barrier; by default step k of a tile
-// is its segment k, 64 packets per wave, with a barrier per step.
+// Segments per wave (1024-packet tiles): wave w of a tile owns the tile's
+// segment w (packets w*256 .. w*256+255) and walks it in four steps of 64
+// packets, so a segment's list is one wave's own forwarded packets in order
+// and no step waits at a barrier for the other waves' counts (one barrier
+// per tile, for the counters). Against step k = segment k with a barrier per
+// step (COPK_SEG_WAVE=0): the driver's command 55,253 / 54,380 / 53,711
+// against 52,950 / 51,901 / 53,188 Mpkt/s, a one-batch post 13.0 against
+// 14.6 us, a lone tile's body 7.4 against 8.7 us (profiles/r05/check23/).
 #ifndef COPK_SEG_WAVE
-#define COPK_SEG_WAVE 0
+#define COPK_SEG_WAVE 1
 #endif
 // the first packet of wave `wave`'s 64 packets in step k, from the tile's base
 template <int PPT>
