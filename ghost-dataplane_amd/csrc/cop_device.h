@@ -1174,6 +1174,18 @@ __device__ __forceinline__ void counters_add(const CopKParams &p, const uint32_t
     }
 }
 
+// One wave's counters (its own Counts, wave-uniform) added by nine of its
+// lanes to shard `shard`: no cross-wave reduction, so no barrier.
+__device__ __forceinline__ void counters_add_wave(const CopKParams &p, const Counts &t, int lane, uint32_t shard)
+{
+    if (lane < 9) {
+        const uint32_t v = lane == 0 ? t.dropfw + t.notv4 : lane == 1 ? t.total - t.notv4 - t.dropfw
+                         : lane == 2 ? t.notv4 : lane == 3 ? t.total : lane == 4 ? t.parse : lane == 5 ? t.noport
+                         : lane == 6 ? t.fwd : lane == 7 ? t.rhit : t.rx;
+        if (v) atomicAdd(&p.counters[(shard % COPK_COUNTER_SHARDS) * 16 + lane], (unsigned long long)v);
+    }
+}
+
 // The segmented-list tile epilogue with the counters folded in (no optional
 // features: COP_CFG_SEG_LISTS without per-rule bins or port statistics).
 // Per (step, wave): ballot of FORWARD; the wave's verdict counters from

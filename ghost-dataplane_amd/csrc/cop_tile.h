@@ -272,6 +272,11 @@ __device__ __forceinline__ void body_prio()
 #ifndef COPK_SEG_WAVE
 #define COPK_SEG_WAVE 1
 #endif
+// experiment builds: with segments per wave, each wave adds its own counters
+// (nine lanes, its own shard) and the tile has no barrier left
+#ifndef COPK_WAVE_COUNTERS
+#define COPK_WAVE_COUNTERS 0
+#endif
 // the first packet of wave `wave`'s 64 packets in step k, from the tile's base
 template <int PPT>
 __device__ __forceinline__ uint32_t step_off(int k, int wave)
@@ -404,8 +409,12 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
                                           B.n);
                 }
                 if (B.fwd_count && lane == 0 && sb < B.n) st_u32<WT>(run, B.fwd_count + sb / COPK_SEG);
-                lds_barrier();   // every wave's counters in s_red
-                counters_add(p, lc.s_red, tid);
+                if (COPK_WAVE_COUNTERS) {
+                    counters_add_wave(p, tot, lane, blockIdx.x * WAVES + (uint32_t)wave);
+                } else {
+                    lds_barrier();   // every wave's counters in s_red
+                    counters_add(p, lc.s_red, tid);
+                }
             }
             return;
         }
