@@ -272,10 +272,13 @@ __device__ __forceinline__ void body_prio()
 #ifndef COPK_SEG_WAVE
 #define COPK_SEG_WAVE 1
 #endif
-// experiment builds: with segments per wave, each wave adds its own counters
-// (nine lanes, its own shard) and the tile has no barrier left
+// With segments per wave, each wave also adds its own counters (nine lanes,
+// a shard of its own) and the tile has no barrier left: the driver's command
+// 55,417 / 56,131 / 55,461 against 52,822 / 52,673 / 53,930 Mpkt/s, three
+// alternating pairs (profiles/r05/check25/; COPK_WAVE_COUNTERS=0 reduces
+// the four waves' counters through LDS behind a barrier)
 #ifndef COPK_WAVE_COUNTERS
-#define COPK_WAVE_COUNTERS 0
+#define COPK_WAVE_COUNTERS 1
 #endif
 // the first packet of wave `wave`'s 64 packets in step k, from the tile's base
 template <int PPT>
