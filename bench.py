@@ -350,8 +350,9 @@ def measure(args, name, rank, world, dev, group, gate, primary):
     pmd = None
 
     # the pool is written once before the kernel starts and never again:
-    # declared (COP_PMD_STATIC_SLOTS), so no tile pays the reuse acquire
-    # (--slots reuse: the default acquire once the ring wraps; always: every tile)
+    # declared (COP_PMD_STATIC_SLOTS), so every tile takes plain loads
+    # (--slots reuse: the default, coherent loads once the ring wraps;
+    # always: coherent loads on every tile)
     pmd_flags = {"static": cg.PMD_STATIC_SLOTS, "reuse": 0, "always": cg.PMD_SYS_ACQUIRE}[args.slots]
 
     def pmd_on():
@@ -574,26 +575,39 @@ def measure(args, name, rank, world, dev, group, gate, primary):
         except Exception:  # noqa: BLE001
             traffic = None
     res["traffic"] = traffic
+    # the poll-mode kernel's PMC traffic per posted batch (tools/pmc_pmd.py:
+    # one kernel lifetime serving exactly K posted batches of this workload)
+    res["traffic_pmd"] = None
+    tp = os.path.join(TRAFFIC_DIR, f"traffic_pmd_{name}_{args.lists}.json")
+    if os.path.exists(tp):
+        try:
+            tj = json.load(open(tp))
+            res["traffic_pmd"] = {"per_batch": tj["hbm_bytes_per_batch"], "batches": tj.get("batches"),
+                                  "kernel": tj.get("kernel"),
+                                  "source": f"bench_traffic/traffic_pmd_{name}_{args.lists}.json"}
+        except Exception:  # noqa: BLE001
+            pass
     return res, ctx
 
 
-def roofline_block(res, world, group, args):
+def roofline_launch_block(res, world, group, args):
+    """The one-shot kernel's roofline: algorithmic bytes per launch of Lb
+    batches / the mean kernel duration (HIP events on the lane's stream around
+    every launch; rocprofv3 --kernel-trace --stats of the same command must
+    agree), PMC traffic per launch (tools/pmc_traffic.py)."""
     achieved, alg_bytes = res["achieved"], res["alg_bytes"]
     ach_min, ach_max, ach_sum = group.min(achieved), group.max(achieved), group.sum(achieved)
     traffic = res["traffic"]
     out = {
+        "engine": "launch",
         "bound": "hbm",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
-        # the timed region itself: algorithmic bytes of the K timed steps
-        # on all GPUs / the timed elapsed / (peak x GPUs) — launch, ramp,
-        # tail and host sync included (frac is the kernel steady state)
-        "frac_timed": round(res["bytes_per_pkt"] * res["total_pkts"] / res["elapsed"] / 1e9 / (HBM_PEAK_GBS * world),
-                            4),
         "traffic": traffic,
         "algorithmic_bytes_per_pkt": round(res["bytes_per_pkt"], 3),
+        "algorithmic_bytes_per_launch": round(alg_bytes),
         "traffic_per_algorithmic": (round(traffic / alg_bytes, 4) if traffic else None),
         "traffic_source": (f"bench_traffic/traffic_{res['name']}_L{res['Lb']}_{args.lists}.json (rocprofv3 PMC, "
                            f"tools/pmc_traffic.py)" if traffic else None),
@@ -603,11 +617,65 @@ def roofline_block(res, world, group, args):
         "all_gpus": {"n": world, "achieved_sum": round(ach_sum, 2), "peak_sum": HBM_PEAK_GBS * world,
                      "frac": round(ach_sum / (HBM_PEAK_GBS * world), 4),
                      "per_gpu_min": round(ach_min, 2), "per_gpu_max": round(ach_max, 2)},
-        "table_probes": res["probes"],
     }
     if "probe" in res:
         out["probe_bound"] = res["probe"]["probe_bound"]
-        out["probe_ceiling"] = res["probe"]
+    return out
+
+
+def roofline_block(res, world, group, args):
+    """The roofline of the engine that produced `value`. For the poll-mode
+    kernel (one launch serves every posted batch, so there is no per-launch
+    duration): the algorithmic bytes of the K timed steps on all GPUs over the
+    timed window, i.e. frac == frac_timed, with the kernel's PMC traffic per
+    posted batch scaled to the same K steps. For one-shot launches: the
+    launch block, plus frac_timed."""
+    bpp = res["bytes_per_pkt"]
+    frac_timed = round(bpp * res["total_pkts"] / res["elapsed"] / 1e9 / (HBM_PEAK_GBS * world), 4)
+    if res["engine"] != "pmd":
+        out = roofline_launch_block(res, world, group, args)
+        out["frac_timed"] = frac_timed
+    else:
+        steps_bytes = bpp * args.steps * res["B"]              # per GPU, per timed window
+        achieved = steps_bytes / res["elapsed"] / 1e9          # max-over-ranks window
+        tp = res.get("traffic_pmd")
+        traffic = tp["per_batch"] * args.steps if tp else None
+        out = {
+            "engine": "pmd",
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frac_timed": frac_timed,
+            "unit_of_work": f"one timed window: {args.steps} posted batches x {res['B']} packets per GPU",
+            "traffic": (round(traffic) if traffic else None),
+            "algorithmic_bytes_per_pkt": round(bpp, 3),
+            "algorithmic_bytes": round(steps_bytes),
+            "traffic_per_algorithmic": (round(traffic / steps_bytes, 4) if traffic else None),
+            "traffic_per_batch": (round(tp["per_batch"]) if tp else None),
+            "traffic_source": (f"{tp['source']} (rocprofv3 PMC FETCH_SIZE / WRITE_SIZE over one kernel lifetime "
+                               f"serving exactly {tp['batches']} posted batches, tools/pmc_pmd.py; the per-batch "
+                               f"bytes x {args.steps} steps)" if tp else None),
+            "kernel": (tp["kernel"] if tp else None),
+            "ms_per_window": round(res["elapsed"] * 1e3, 6),
+            "timing": "host CLOCK_MONOTONIC around post -> every batch complete (the poll-mode kernel's one "
+                      "launch serves every post: no per-launch kernel time exists; rocprofv3 sees one lifetime "
+                      "dispatch)",
+        }
+    out["table_probes"] = res["probes"]
+    if "probe" in res:
+        pr = dict(res["probe"])
+        if res["engine"] == "pmd":
+            # the poll-mode rate over the timed window against the same box's
+            # random-probe ceiling (the one-shot kernel's is roofline_launch's)
+            g = pr["per_pkt"] * args.steps * res["B"] / res["elapsed"] / 1e9
+            pr["timed_gprobes_s"] = round(g, 2)
+            pr["probe_bound_timed"] = round(g / pr["ceiling_gprobes_s"], 4)
+            out["probe_bound"] = pr["probe_bound_timed"]
+        else:
+            out["probe_bound"] = pr["probe_bound"]
+        out["probe_ceiling"] = pr
     return out
 
 
@@ -677,8 +745,9 @@ def main():
                          "across every rank (configs[4]))")
     ap.add_argument("--slots", default="static", choices=("static", "reuse", "always"),
                     help="poll-mode slot declaration: static = the pool is written once before the start "
-                         "(COP_PMD_STATIC_SLOTS, no acquire); reuse = the default of cop_pmd_start (a system-scope "
-                         "acquire per tile once the ring wraps); always = an acquire on every tile")
+                         "(COP_PMD_STATIC_SLOTS, plain loads); reuse = the default of cop_pmd_start "
+                         "(system-coherent sc0 sc1 loads once the ring wraps); always = coherent loads on every "
+                         "tile (COP_PMD_SYS_ACQUIRE)")
     ap.add_argument("--fw-form", default="dir", choices=("dir", "bkt"),
                     help="firewall tables too large for LDS (1M rules): DIR-24-8 image, or the bucketed intervals "
                          "keyed by rule id (COP_CFG_FW_BKT)")
@@ -793,13 +862,13 @@ def main():
     if not W["imix"] and not args.quick:
         ceiling = box_ceiling(res["d_pkts"].addr, P * B, res["d_res"].addr)
 
+    # the roofline of the engine behind `value` (config.engine), and the
+    # one-shot kernel's beside it (its HIP-event launch time is what rocprofv3
+    # --kernel-trace --stats of this command reports)
     roof = roofline_block(res, world, group, args)
-    # which engine the roofline's kernel time comes from (`value` may come
-    # from the poll-mode kernel: config.engine; its own roofline is
-    # roofline_pmd)
-    roof["engine"] = "launch"
+    roof_launch = roof if res["engine"] != "pmd" else roofline_launch_block(res, world, group, args)
     if ceiling is not None:
-        roof["box_ceiling"] = {
+        roof_launch["box_ceiling"] = {
             "what": "same pool, same process: read each 64 B slot + write an 8 B record, no classification "
                     "(tools/ceiling.hip: the best of grid-stride copies and per-wave LDS-DMA rings)",
             "best_pattern": ceiling[1], "achieved": round(ceiling[0], 2), "unit": "GB/s",
@@ -852,6 +921,8 @@ def main():
         "roofline": roof,
         "cpu_baseline": None,
     }
+    if roof_launch is not roof:
+        out["roofline_launch"] = roof_launch
     if single_batch:
         out["single_batch_latency"] = single_batch
     if "pmd_info" in res:
@@ -862,28 +933,12 @@ def main():
         if "dynamic_tiles" in pi:
             dt = pi["dynamic_tiles"]
             dt["steady_frac"] = round(dt["steady_mpkt_s"] * 1e6 * res["bytes_per_pkt"] / 1e9 / HBM_PEAK_GBS, 4)
+        if res.get("traffic_pmd"):
+            tp = res["traffic_pmd"]
+            pi["traffic_per_batch"] = round(tp["per_batch"])
+            pi["traffic_per_algorithmic"] = round(tp["per_batch"] / (res["bytes_per_pkt"] * B), 4)
+            pi["traffic_source"] = tp["source"]
         out["pmd"] = pi
-        # the roofline of the engine that produced `value` when it is the
-        # poll-mode kernel: algorithmic bytes of its steady 1024-batch post
-        # over the host-timed post -> done, and its PMC traffic per posted
-        # batch (a rocprofv3 pass over a kernel lifetime that served exactly
-        # K posted batches and was stopped at once: tools/pmc_pmd.py)
-        ach = pi["steady_mpkt_s"] * 1e6 * res["bytes_per_pkt"] / 1e9
-        rp = {"engine": "pmd", "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-              "frac": round(ach / HBM_PEAK_GBS, 4), "batches": pi["steady_batches"], "ms": pi["steady_ms"],
-              "algorithmic_bytes_per_pkt": round(res["bytes_per_pkt"], 3), "traffic_per_batch": None,
-              "traffic_per_algorithmic": None, "traffic_source": None}
-        tp = os.path.join(TRAFFIC_DIR, f"traffic_pmd_{res['name']}_{args.lists}.json")
-        if os.path.exists(tp):
-            try:
-                tj = json.load(open(tp))
-                rp["traffic_per_batch"] = tj["hbm_bytes_per_batch"]
-                rp["traffic_per_algorithmic"] = round(tj["hbm_bytes_per_batch"] / (res["bytes_per_pkt"] * B), 4)
-                rp["traffic_source"] = (f"bench_traffic/traffic_pmd_{res['name']}_{args.lists}.json (rocprofv3 "
-                                        f"PMC over {tj.get('batches')} posted batches, tools/pmc_pmd.py)")
-            except Exception:  # noqa: BLE001
-                pass
-        out["roofline_pmd"] = rp
     if "reduce_info" in res:
         out["counter_reduce"] = res["reduce_info"]
     if allreduce_check:
@@ -897,6 +952,7 @@ def main():
         try:
             sres, sctx = measure(args, sname, rank, world, dev, group, gate, primary=False)
             sroof = roofline_block(sres, world, group, args)
+            sroof_launch = roofline_launch_block(sres, world, group, args) if sres["engine"] == "pmd" else None
             blk = {
                 "description": sres["W"]["desc"], "value": round(sres["value"], 3), "unit": "Mpkt/s",
                 "steps": args.steps, "warmup": args.warmup,
@@ -908,6 +964,8 @@ def main():
                 "pkt_layout": "imix slab + u32 offsets" if sres["W"]["imix"] else "64B slots",
                 "route_form": args.route_form, "fw_form": args.fw_form if sres["W"]["fw"] > 8192 else "lds-intervals",
                 "rule_counters": sres["rc_on"], "roofline": sroof}
+            if sroof_launch is not None:
+                blk["roofline_launch"] = sroof_launch
             if sres["rc_on"]:
                 blk["rccl_init"] = group.gather_obj(sres["coll"])
             if "reduce_info" in sres:

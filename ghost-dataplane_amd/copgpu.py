@@ -87,7 +87,7 @@ class TraceOpts(Structure):
 class PmdInfo(Structure):
     _fields_ = [("workers", c_uint32), ("workers_per_cu", c_uint32), ("tiles_per_batch", c_uint32),
                 ("packets_per_tile", c_uint32), ("launches", c_uint32), ("state", c_uint32),
-                ("posted", c_uint64), ("completed", c_uint64)]
+                ("posted", c_uint64), ("completed", c_uint64), ("slot_loads", c_uint32), ("kernel", c_uint32)]
 
 
 class NfStats(Structure):
@@ -740,7 +740,12 @@ class Pmd:
     def info(self) -> dict:
         i = PmdInfo()
         _check(lib().cop_pmd_info(self.handle, byref(i)), self.ctx, "pmd_info")
-        return {k: getattr(i, k) for k, _ in PmdInfo._fields_}
+        d = {k: getattr(i, k) for k, _ in PmdInfo._fields_}
+        k = d["kernel"]
+        # the instantiation's template arguments, as rocprofv3 names the kernel
+        d["kernel_name"] = (f"cop_pmd<{k & 15}, {(k >> 4) & 15}, {(k >> 8) & 15}, {d['packets_per_tile'] // 256}, "
+                            f"{'true' if (k >> 12) & 1 else 'false'}>")
+        return d
 
     def stop(self):
         if self.handle and self.handle.value:

@@ -65,9 +65,11 @@ __device__ __forceinline__ __attribute__((unused)) unsigned long long ticket_tak
 }
 
 // the bucketed route form at 4 packets per lane sits just above 96 VGPRs:
-// held to 96, it runs 5 waves per SIMD instead of 4
+// held to 96, it runs 5 waves per SIMD instead of 4. Not with the bucketed
+// firewall: held to 96 those parts spill (44-144 bytes per lane of scratch,
+// -Rpass-analysis=kernel-resource-usage), so they keep 4 waves (103-123 VGPRs)
 template <int FW, int LPM, int LAY, int PPT, bool EXT>
-__global__ __launch_bounds__(BLOCK, EXT ? 4 : (LPM == COPK_TBL_BKT && PPT == 4) ? 5 : COPK_WAVES_PER_EU) void
+__global__ __launch_bounds__(BLOCK, EXT ? 4 : (LPM == COPK_TBL_BKT && FW != COPK_TBL_BKT && PPT == 4) ? 5 : COPK_WAVES_PER_EU) void
 cop_pipeline(const CopKParams p)
 {
     const Opt o = EXT ? opt_all(p) : Opt{0u, 0u, 0u, nullptr};
@@ -160,13 +162,14 @@ hipError_t launch_lpm(const CopKParams &p, int lpm, int imix, int ppt, uint32_t 
         if (lpm == COPK_TBL_DIR) return launch_imix<FW, COPK_TBL_DIR>(p, imix, ppt, grid, lds, s);
         if (lpm == COPK_TBL_BKT) return launch_imix<FW, COPK_TBL_BKT>(p, imix, ppt, grid, lds, s);
         if (lpm == COPK_TBL_OFF) return launch_imix<FW, COPK_TBL_OFF>(p, imix, ppt, grid, lds, s);
-        return hipErrorInvalidValue;
+        return hipErrorInvalidValue;   // fill_launch maps IVT / TRIE routes to DIR-24-8 here
+    } else {
+        if (lpm == COPK_TBL_IVT) return launch_imix<FW, COPK_TBL_IVT>(p, imix, ppt, grid, lds, s);
+        if (lpm == COPK_TBL_DIR) return launch_imix<FW, COPK_TBL_DIR>(p, imix, ppt, grid, lds, s);
+        if (lpm == COPK_TBL_TRIE) return launch_imix<FW, COPK_TBL_TRIE>(p, imix, ppt, grid, lds, s);
+        if (lpm == COPK_TBL_BKT) return launch_imix<FW, COPK_TBL_BKT>(p, imix, ppt, grid, lds, s);
+        return launch_imix<FW, COPK_TBL_OFF>(p, imix, ppt, grid, lds, s);
     }
-    if (lpm == COPK_TBL_IVT) return launch_imix<FW, COPK_TBL_IVT>(p, imix, ppt, grid, lds, s);
-    if (lpm == COPK_TBL_DIR) return launch_imix<FW, COPK_TBL_DIR>(p, imix, ppt, grid, lds, s);
-    if (lpm == COPK_TBL_TRIE) return launch_imix<FW, COPK_TBL_TRIE>(p, imix, ppt, grid, lds, s);
-    if (lpm == COPK_TBL_BKT) return launch_imix<FW, COPK_TBL_BKT>(p, imix, ppt, grid, lds, s);
-    return launch_imix<FW, COPK_TBL_OFF>(p, imix, ppt, grid, lds, s);
 }
 
 } // namespace

@@ -642,13 +642,14 @@ hipError_t pmd_lpm(const CopKPmd *p, int lpm, int lay, int ppt, int ext, uint32_
         if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);
         if (lpm == COPK_TBL_BKT) return pmd_lay<FW, COPK_TBL_BKT>(p, lay, ppt, ext, lds, s, occ);
         if (lpm == COPK_TBL_OFF) return pmd_lay<FW, COPK_TBL_OFF>(p, lay, ppt, ext, lds, s, occ);
-        return hipErrorInvalidValue;
+        return hipErrorInvalidValue;   // fill_launch maps IVT / TRIE routes to DIR-24-8 here
+    } else {
+        if (lpm == COPK_TBL_IVT) return pmd_lay<FW, COPK_TBL_IVT>(p, lay, ppt, ext, lds, s, occ);
+        if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);
+        if (lpm == COPK_TBL_TRIE) return pmd_lay<FW, COPK_TBL_TRIE>(p, lay, ppt, ext, lds, s, occ);
+        if (lpm == COPK_TBL_BKT) return pmd_lay<FW, COPK_TBL_BKT>(p, lay, ppt, ext, lds, s, occ);
+        return pmd_lay<FW, COPK_TBL_OFF>(p, lay, ppt, ext, lds, s, occ);
     }
-    if (lpm == COPK_TBL_IVT) return pmd_lay<FW, COPK_TBL_IVT>(p, lay, ppt, ext, lds, s, occ);
-    if (lpm == COPK_TBL_DIR) return pmd_lay<FW, COPK_TBL_DIR>(p, lay, ppt, ext, lds, s, occ);
-    if (lpm == COPK_TBL_TRIE) return pmd_lay<FW, COPK_TBL_TRIE>(p, lay, ppt, ext, lds, s, occ);
-    if (lpm == COPK_TBL_BKT) return pmd_lay<FW, COPK_TBL_BKT>(p, lay, ppt, ext, lds, s, occ);
-    return pmd_lay<FW, COPK_TBL_OFF>(p, lay, ppt, ext, lds, s, occ);
 #endif
 }
 

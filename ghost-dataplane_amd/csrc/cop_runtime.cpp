@@ -886,10 +886,10 @@ static int choose_ppt(const cop_ctx *c, uint64_t total, bool imix)
     int ppt = 1;
     if (total >= (uint64_t)COPK_BLOCK * 8 * c->ncu) ppt = imix ? 4 : 8;
     else if (total >= (uint64_t)COPK_BLOCK * 4 * c->ncu) ppt = 4;
-    // the bucketed route form reads 64 bytes of pairs per packet in one
-    // round: at 8 packets per lane that needs 195 VGPRs (2 waves per SIMD),
-    // at 4, 98 (4 waves)
-    if (c->lpm.bidx && ppt > 4) ppt = 4;
+    // the bucketed forms read 64 bytes of pairs per packet in one round: at
+    // 8 packets per lane that needs 195 VGPRs (2 waves per SIMD), at 4, 98
+    // (4 waves); the firewall's bucketed form (COP_CFG_FW_BKT) the same
+    if ((c->lpm.bidx || c->fw.bidx) && ppt > 4) ppt = 4;
     if (c->ppt_override) ppt = c->ppt_override;
     return ppt;
 }
@@ -947,6 +947,18 @@ static int fill_launch(cop_ctx *c, CopKParams &p, int ppt, int *fw_mode_out, int
         if ((lpm_mode == COPK_TBL_IVT || lpm_mode == COPK_TBL_TRIE) && c->lpm.tbl24) lpm_mode = COPK_TBL_DIR;
         else if (fw_mode == COPK_TBL_IVT && c->fw.tbl24) fw_mode = COPK_TBL_DIR;
         else return set_err(c, -E2BIG, "tables exceed LDS (%u bytes)", lds_need(fw_mode, lpm_mode));
+    }
+    // The bucketed firewall's kernel parts are built for the route forms that
+    // large tables take (DIR-24-8, bucketed) and for no route stage: a route
+    // table small enough for LDS, or in the trie form, is looked up in its
+    // DIR-24-8 image beside it (same results). Only the empty route table has
+    // no image.
+    if (fw_mode == COPK_TBL_BKT && (lpm_mode == COPK_TBL_IVT || lpm_mode == COPK_TBL_TRIE)) {
+        if (!c->lpm.tbl24)
+            return set_err(c, -EINVAL,
+                           "bucketed firewall (COP_CFG_FW_BKT) with the route stage on needs a route table "
+                           "(cop_set_route_lpm)");
+        lpm_mode = COPK_TBL_DIR;
     }
     p.fw_m = fw_mode == COPK_TBL_IVT ? c->fw.m : 0;
     p.fw_ib = c->fw.ib;
@@ -2219,6 +2231,17 @@ static void pmd_size(cop_pmd *m)
                 m->P.sys_acquire = 3;
         }
         (void)hipGetLastError();   // (an unregistered pointer leaves an error behind)
+        // Mode 4 trusts a slot's first read in a launch, which holds only if
+        // no read of another slot brought one of its cache lines in earlier:
+        // slots (and IMIX offset arrays) must start on 128-byte L2 lines. A
+        // ring whose slots share lines (e.g. 4097 packets 64 bytes apart per
+        // slot) takes coherent loads on every tile (mode 3).
+        for (uint32_t q = 0; q < m->n_rings && m->P.sys_acquire == 4u; q++) {
+            const CopKRing &r = m->P.rings[q];
+            bool lined = (uintptr_t)r.pkts % 128u == 0 && r.pkts_slot_bytes % 128u == 0;
+            if (r.offsets) lined = lined && (uintptr_t)r.offsets % 128u == 0 && (r.offsets_slot_words * 4u) % 128u == 0;
+            if (!lined) m->P.sys_acquire = 3;
+        }
     }
     if (const char *e = getenv("COP_PMD_ACQUIRE")) m->P.sys_acquire = std::min(4u, (uint32_t)atoi(e));   // A/B runs
     // tests: a tile that never runs, so its successors' look-back gives up
@@ -2390,6 +2413,17 @@ int cop_pmd_start_rings_stages(cop_ctx *c, const cop_batch_ring *rings, uint32_t
         if (x->results_slot < x->n || (x->fwd_idx && x->fwd_slot < (uint64_t)x->n * lists))
             return set_err(c, -EINVAL, "pmd: slot sizes smaller than n (x ports with demux)");
         if (int rc = check_seg_ring(c, x, seg)) return rc;
+        // the coherent slot loads (every mode but COP_PMD_STATIC_SLOTS) take
+        // 31-bit byte offsets from the slot's base (a buffer resource,
+        // cop_device.h sys_rsrc): a slot's packets must lie within its first
+        // 2 GiB, where an IMIX offset can reach anywhere in the slot
+        const uint64_t span = imix ? x->pkts_slot_bytes + x->data_off + 64u
+                                   : (uint64_t)x->n * x->stride + x->data_off + 64u;
+        if (!(flags & COP_PMD_STATIC_SLOTS) && span > 0x7FFFFFFFull)
+            return set_err(c, -EINVAL,
+                           "pmd: slots span %llu bytes; coherent slot loads reach 2 GiB (COP_PMD_STATIC_SLOTS for "
+                           "slots written once)",
+                           (unsigned long long)span);
         wide = wide && ((uintptr_t)x->results & 15) == 0 && (x->results_slot & 1) == 0;
     }
     if (int rc = sync_lanes(c)) return rc;
@@ -2703,6 +2737,9 @@ int cop_pmd_info(const cop_pmd *m, cop_pmd_info_t *out)
     out->packets_per_tile = COPK_BLOCK * (uint32_t)m->ppt;
     out->launches = m->launches.load();
     out->state = m->h_state[0];
+    out->slot_loads = m->P.sys_acquire;
+    out->kernel = (uint32_t)m->fw_mode | (uint32_t)m->lpm_mode << 4 | (uint32_t)m->layout << 8 |
+                  (uint32_t)(m->ext ? 1 : 0) << 12;
     out->posted = out->completed = 0;
     for (uint32_t r = 0; r < m->n_rings; r++) {   // every ring's batches
         out->posted += m->ring[r].posted.load();

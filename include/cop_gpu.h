@@ -431,6 +431,16 @@ typedef struct cop_pmd_info_t {
     uint32_t launches;         /* 1 + relaunches after idle exits */
     uint32_t state;            /* 0 running, 1 stopped, 2 left idle, 3 aborted, 4 paused */
     uint64_t posted, completed; /* summed over the rings */
+    uint32_t slot_loads;       /* how tiles read their slots: 0 plain (COP_PMD_STATIC_SLOTS),
+                                  3 system-coherent loads every tile (COP_PMD_SYS_ACQUIRE,
+                                  host-memory rings, or slots not on 128-byte lines),
+                                  4 coherent loads once the ring wraps (default); 1 and 2
+                                  (acquires) only through $COP_PMD_ACQUIRE A/B runs */
+    uint32_t kernel;           /* the kernel instantiation serving the rings,
+                                  cop_pmd<fw, route, layout, ppt, ext>: fw table form | route form << 4
+                                  | layout << 8 | ext << 12 (forms: 0 off, 1 LDS intervals, 2 DIR-24-8,
+                                  3 trie, 4 bucketed; layouts: 0 slots, 1 IMIX, 2 coalesced 64 B,
+                                  3 16-byte records; ppt = packets_per_tile / 256) */
 } cop_pmd_info_t;
 int cop_pmd_info(const cop_pmd *pmd, cop_pmd_info_t *out);
 /* Complete everything posted, stop the kernel, free. */

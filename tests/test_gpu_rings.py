@@ -166,6 +166,26 @@ def test_rings_reject_mismatched_geometry(gpu_ctx_factory):
         ctx.pmd_start([a.ring] * 9)
 
 
+def test_rings_over_2gib_need_static_slots(gpu_ctx_factory):
+    """coherent slot loads take 31-bit offsets from the slot's
+    base, so a ring whose batch spans 2 GiB or more (1M packets 2176 bytes
+    apart, an mbuf pool's stride) is refused unless its slots are declared
+    static (plain 64-bit addressing). Nothing is launched: the geometry is
+    checked before the kernel starts."""
+    rules = fw1k()
+    n = 1 << 20
+    ctx = gpu_ctx_factory(stages=S | F, max_batch=n)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    dp = ctx.alloc(1 << 20)   # the descriptor is only validated
+    dr = ctx.alloc(n * 8)
+    ring = cg.make_ring(dp, 1, n, dr, n * 2176, stride=2176)
+    with pytest.raises(cg.CopError) as ei:
+        ctx.pmd_start(ring)
+    assert ei.value.code == -22
+    with pytest.raises(cg.CopError):
+        ctx.pmd_start(ring, cg.PMD_SYS_ACQUIRE)
+
+
 @pytest.mark.parametrize("stages", [F, S | F])
 def test_hdr16_rings_variable_n(gpu_ctx_factory, stages):
     """The drop-in's kernel shape through the batch-ring API: two rings of
@@ -205,11 +225,12 @@ def test_slots_rewritten_between_batches(gpu_ctx_factory, flags):
     """A producer that rewrites ring slots between batches (here the host,
     by cop_memcpy_h2d copies into HBM; on a real deployment a NIC, as the
     reference's fast path refills its rings, switch.c:463-470): each tile
-    acquires before its loads once the ring has wrapped (the default: flags
-    0 goes through the single-ring cop_pmd_start) or on every tile
-    (COP_PMD_SYS_ACQUIRE), so a slot's new packets are read, never the
-    previous batch's that a CU or L2 may still hold. Eight generations
-    through a two-slot ring, records and lists per batch."""
+    reads its slot with system-coherent (sc0 sc1) loads once the ring has
+    wrapped (the default: flags 0 goes through the single-ring
+    cop_pmd_start) or on every tile (COP_PMD_SYS_ACQUIRE), so a slot's new
+    packets are read, never the previous batch's that a CU or L2 may still
+    hold. Eight generations through a two-slot ring, records and lists per
+    batch."""
     rules = fw1k()
     ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
     ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
@@ -231,6 +252,44 @@ def test_slots_rewritten_between_batches(gpu_ctx_factory, flags):
             assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"generation {g}"
             assert np.array_equal(seg_to_dense(fwd, cnt, B), fo), f"generation {g} list"
         assert m.info()["launches"] == 1   # served by one launch: no relaunch invalidated the caches
+        assert m.info()["slot_loads"] == (3 if flags else 4)
+
+
+def test_unaligned_slots_rewritten_between_batches(gpu_ctx_factory):
+    """slots that do not start on 128-byte lines (4097 packets 64
+    bytes apart: a slot's last packet shares its line with the next slot's
+    first). Reading slot s's last packet caches the first line of slot s+1
+    before the producer rewrites it, so a first-lap plain load of slot s+1
+    could see stale bytes; such a ring takes coherent loads on every tile
+    (slot_loads 3). Nine generations through three slots, every slot
+    rewritten before its first post, records and lists per batch."""
+    rules = fw1k()
+    ctx = gpu_ctx_factory(stages=S | F, flags=cg.CFG_SEG_LISTS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    fw, _ = oracle_tables(rules)
+    B, P = 4097, 3
+    assert (B * 64) % 128 != 0
+    gens = [cg.gen_trace(0x5EED7A00 + g, B, rules) for g in range(9)]
+    # the slots hold an older generation when the kernel starts; lists of a
+    # slot start 16-byte aligned (fwd_slot 4100)
+    rg = SegRing(ctx, np.concatenate([cg.gen_trace(0x5EED7AF0, B, rules)] * P), B, P)
+    FS = 4100
+    rg.df = ctx.alloc(FS * P * 4)
+    rg.ring = cg.make_ring(rg.dp, P, B, rg.dr, B * 64, fwd_idx=rg.df, fwd_slot=FS, fwd_count=rg.dc)
+    with ctx.pmd_start(rg.ring) as m:
+        assert m.info()["slot_loads"] == 3
+        for g in range(9):
+            s_ = g % P
+            rg.dp.upload(gens[g], s_ * B * 64)
+            m.post(1)
+            m.wait()
+            res = rg.dr.download(cg.RESULT_DT, B * P)[s_ * B:(s_ + 1) * B]
+            fwd = rg.df.download(np.uint32, FS * P)[s_ * FS:s_ * FS + B]
+            cnt = rg.dc.download(np.uint32, P * nseg(B))[s_ * nseg(B):(s_ + 1) * nseg(B)]
+            ro, fo = oracle_batch(gens[g], B, S | F, fw)
+            assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"generation {g}"
+            assert np.array_equal(seg_to_dense(fwd, cnt, B), fo), f"generation {g} list"
+        assert m.info()["launches"] == 1
 
 
 @pytest.mark.parametrize("flags", [0, cg.PMD_DYNAMIC_TILES])
@@ -286,6 +345,7 @@ def test_static_slots_contradicts_acquire(gpu_ctx_factory):
         ctx.pmd_start(rg.ring, cg.PMD_SYS_ACQUIRE | cg.PMD_STATIC_SLOTS)
     with ctx.pmd_start(rg.ring, cg.PMD_STATIC_SLOTS) as m:   # the bench's declaration
         m.run(4)
+        assert m.info()["slot_loads"] == 0
     assert ctx.counters()["rx"] == 4 * 65536
 
 

@@ -189,3 +189,47 @@ def test_fw_bkt_poll_mode_with_rule_counters(gpu_ctx_factory):
         hits += h * np.uint64(len(range(s, N, P)))   # slot s served batches s, s + P, ...
     assert ctx.counters()["rx"] == N * B
     assert np.array_equal(ctx.rule_counters(), hits)
+
+
+@pytest.mark.parametrize("route", ["lds", "trie", "empty"])
+def test_fw_bkt_beside_small_or_trie_routes(gpu_ctx_factory, route):
+    """the bucketed firewall's kernel parts are built for the
+    large route forms only (DIR-24-8, bucketed). A route table small enough
+    for LDS (1k routes) or in the trie form (CFG_LPM_TRIE) is looked up in
+    its DIR-24-8 image beside it, with the oracle's results, in one-shot
+    launches and in the poll-mode kernel; with no route table at all the
+    launch fails with -EINVAL and a message, not an opaque -EIO."""
+    fw_rules = cg.gen_rules(0x5EED1079, 20000, cg.GEN_FW, 0)
+    fwt = cg.LpmTable(fw_rules, 20000, 1 << 16, False)
+    assert len(fwt.intervals()[0]) > 8192
+    routes = cg.gen_rules(0x5EED2097, 1000 if route == "lds" else 30000, cg.GEN_ROUTES, 0)
+    flags = cg.CFG_FW_BKT | (cg.CFG_LPM_TRIE if route == "trie" else 0)
+    ctx = gpu_ctx_factory(stages=S | F | L, flags=flags)
+    ctx.set_fw_table(fwt)
+    n = 65536
+    pk = cg.gen_trace(0x5EED0081, n, fw_rules, routes)
+    if route == "empty":
+        with pytest.raises(cg.CopError) as ei:
+            gpu_run(ctx, pk, n)
+        assert ei.value.code == -22
+        return
+    rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
+    ctx.set_route_lpm(rtt)
+    assert ctx.route_form() == ("trie" if route == "trie" else "lds")   # the launch maps it to DIR-24-8
+    ofw = orc.OracleLpm(20000, 1 << 16)
+    ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"], stop_at_error=False)
+    ort = orc.OracleLpm(1 << 20, 1 << 16)
+    ort.setup(routes["ip"], routes["depth"], routes["next_hop"], stop_at_error=False)
+    ro, fo, _ = orc.process(pk, n, stages=S | F | L, fw=ofw, route=ort)
+    assert ((ro["flags"] & 1) == 1).mean() > 0.3      # the route stage hits
+    rg, fg, _ = gpu_run(ctx, pk, n, batches=2)
+    assert_parity(rg, fg, ro, fo)
+    dp = ctx.alloc(pk.nbytes)
+    dp.upload(pk)
+    dr = ctx.alloc(n * 8)
+    dr.fill(0xEE)
+    ring = cg.make_ring(dp, 1, n, dr, n * 64)
+    with ctx.pmd_start(ring) as m:
+        m.run(2)
+    res = dr.download(cg.RESULT_DT, n)
+    assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))

@@ -58,6 +58,21 @@ for s in "$@"; do
       step 200 "$out/pmd_pmc_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/pmd_write" -o pmd --output-format csv -- python3 "$R/tools/pmc_pmd.py" run --batches 1024
       step 200 "$out/mb_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/mb_fetch" -o mb --output-format csv -- "$R/tools/membench"
       step 200 "$out/mb_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/mb_write" -o mb --output-format csv -- "$R/tools/membench" ;;
+    pmc_all)
+      # every workload of the line, both engines: poll-mode FETCH_SIZE /
+      # WRITE_SIZE over one lifetime serving exactly K posted batches
+      # (tools/pmc_pmd.py), one-shot passes over bench.py --quick of that
+      # workload alone; membench calibration once (reduce on the CPU with
+      # tools/pmc_pmd.py reduce and tools/pmc_traffic.py)
+      for wk in ${PMC_WORKLOADS:-fw1k:1024 fw_lpm:1024 fw_lpm_imix:384 fw_lpm_1m:384}; do
+        w=${wk%%:*}; k=${wk##*:}
+        step 300 "$out/pmd_${w}_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/pmd_${w}_fetch" -o pmd --output-format csv -- python3 "$R/tools/pmc_pmd.py" run --workload "$w" --batches "$k"
+        step 300 "$out/pmd_${w}_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/pmd_${w}_write" -o pmd --output-format csv -- python3 "$R/tools/pmc_pmd.py" run --workload "$w" --batches "$k"
+        step 400 "$out/os_${w}_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/os_${w}_fetch" -o os --output-format csv -- python3 "$R/bench.py" --quick --workload "$w" --steps 20 --warmup 5 --secondary none --no-cpu
+        step 400 "$out/os_${w}_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/os_${w}_write" -o os --output-format csv -- python3 "$R/bench.py" --quick --workload "$w" --steps 20 --warmup 5 --secondary none --no-cpu
+      done
+      step 200 "$out/mb_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/mb_fetch" -o mb --output-format csv -- "$R/tools/membench"
+      step 200 "$out/mb_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/mb_write" -o mb --output-format csv -- "$R/tools/membench" ;;
     pmc_oneshot)
       # the one-shot kernel's PMC passes over the driver's command (reduce
       # here with tools/pmc_traffic.py and the membench passes of pmc_pmd)

@@ -10,7 +10,7 @@ FETCH_SIZE / WRITE_SIZE (separate passes); divided by K they are the
 traffic per batch (the start-up census and table staging included, a few
 KiB).
 
-  run      [--workload fw1k|fw_lpm] [--batches K] [--lists seg|dense]
+  run      [--workload fw1k|fw_lpm|fw_lpm_imix|fw_lpm_1m] [--batches K] [--lists seg|dense]
            the workload, meant to run under rocprofv3 --pmc
   reduce   <fetch.csv> <write.csv> <fetch_mb.csv> <write_mb.csv> <out.json> --batches K [--pkts-per-batch B]
            bytes per batch, read factor calibrated on tools/membench as in
@@ -28,32 +28,61 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
 def run(a):
+    """Build the workload exactly as bench.py's measure() does (same seeds,
+    tables, context flags, batch layout and slot declaration), then one
+    kernel lifetime that serves exactly K posted batches."""
     import copgpu as cg
-    S, F, L = cg.STAGE_PARSE, cg.STAGE_FW, cg.STAGE_LPM
-    B = 65536
-    rules = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
-    routes = cg.gen_rules(0x5EED2004, 100000, cg.GEN_ROUTES, 0) if a.workload == "fw_lpm" else None
+    import copdist
+    sys.path.insert(0, ROOT)
+    from bench import WORKLOADS
+    W = WORKLOADS[a.workload]
+    B, cid = W["batch"], W["cid"]
+    rc_on = bool(W.get("rule_counters"))
+    fw_rules = cg.gen_rules(0x5EED1000 + cid, W["fw"], cg.GEN_FW, 20 if W["fw"] <= 1000 else 0)
+    routes = cg.gen_rules(0x5EED2000 + cid, W["routes"], cg.GEN_ROUTES, 0) if W["routes"] else None
     seg = a.lists == "seg"
-    ctx = cg.Context(device=0, stages=(S | F | L) if routes is not None else (S | F), max_batch=B, max_batches=32,
-                     flags=cg.CFG_SEG_LISTS if seg else 0)
-    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    ctx = cg.Context(device=0, stages=W["stages"], max_batch=B, max_batches=32,
+                     flags=(cg.CFG_SEG_LISTS if seg else 0) | (cg.CFG_RULE_COUNTERS if rc_on else 0))
+    if W["fw"] <= 1024:
+        ctx.set_fw_table(cg.LpmTable(fw_rules, 1024, 24, True))
+    else:
+        ctx.set_fw_table(cg.LpmTable(fw_rules, W["fw"], 1 << 20, False))
     if routes is not None:
-        ctx.set_route_lpm(cg.LpmTable(routes, 100000, 1 << 20, False))
+        ctx.set_route_lpm(cg.LpmTable(routes, max(W["routes"], 1), 1 << 20, False))
     P = a.batches
-    dp = ctx.alloc(P * B * 64)
-    for i in range(0, P, 16):
-        k = min(16, P - i)
-        dp.upload(cg.gen_trace(0x5EED0002 + i, k * B, rules, routes), i * B * 64)
+    if W["imix"]:
+        slab, offs = cg.gen_imix(copdist.shard_seed(0x5EED0000 + cid, 0), B, fw_rules, routes)
+        per_batch = slab.nbytes + offs.nbytes
+    else:
+        per_batch = B * 64
+    dp = ctx.alloc(P * per_batch)
+    if W["imix"]:
+        for i in range(P):
+            dp.upload(slab, i * per_batch)
+            dp.upload(offs, i * per_batch + slab.nbytes)
+    else:
+        for i in range(0, P, 16):
+            k = min(16, P - i)
+            dp.upload(cg.gen_trace(copdist.shard_seed(0x5EED0000 + cid, 0, i), k * B, fw_rules, routes),
+                      i * per_batch)
     dr = ctx.alloc(P * B * 8)
     df = ctx.alloc(P * B * 4)
     dc = ctx.alloc(P * ((B + cg.SEG_PKTS - 1) // cg.SEG_PKTS if seg else 1) * 4 + 16)
-    ring = cg.make_ring(dp, P, B, dr, B * 64, stride=64, fwd_idx=df, fwd_count=dc)
-    m = ctx.pmd_start(ring)
+    if W["imix"]:
+        ring = cg.make_ring(dp, P, B, dr, per_batch, offsets=dp.addr + slab.nbytes,
+                            offsets_slot_words=per_batch // 4, fwd_idx=df, fwd_count=dc)
+    else:
+        ring = cg.make_ring(dp, P, B, dr, per_batch, stride=64, fwd_idx=df, fwd_count=dc)
+    # bench.py's pool is written once before the kernel starts (--slots static)
+    m = ctx.pmd_start(ring, cg.PMD_STATIC_SLOTS)
     m.post(P)
     m.wait()
+    info = m.info()
     m.stop()
     c = ctx.counters()
-    print(json.dumps({"workload": a.workload, "batches": P, "rx": int(c["rx"]), "ok": int(c["rx"]) == P * B}))
+    print(json.dumps({"workload": a.workload, "batches": P, "pkts_per_batch": B, "rx": int(c["rx"]),
+                      "forward": int(c["forward"]), "ok": int(c["rx"]) == P * B,
+                      "workers": info["workers"], "packets_per_tile": info["packets_per_tile"]}))
     ctx.close()
 
 
@@ -89,7 +118,7 @@ def main():
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="cmd", required=True)
     r = sub.add_parser("run")
-    r.add_argument("--workload", default="fw1k", choices=("fw1k", "fw_lpm"))
+    r.add_argument("--workload", default="fw1k", choices=("fw1k", "fw_lpm", "fw_lpm_imix", "fw_lpm_1m"))
     r.add_argument("--batches", type=int, default=1024)
     r.add_argument("--lists", default="seg", choices=("seg", "dense"))
     d = sub.add_parser("reduce")

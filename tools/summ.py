@@ -9,10 +9,12 @@ for f in sys.argv[1:]:
             continue
         d = json.loads(line)
         r = d["roofline"]
-        bc = r.get("box_ceiling") or {}
+        rl = d.get("roofline_launch", r)
+        bc = rl.get("box_ceiling") or {}
         print(f"{f}: {d['config']['workload']} {d['config'].get('engine')} value {d['value']:.1f} runs_us "
-              f"{[round(x * 1e3, 1) for x in d['runs_ms']]} frac {r['frac']} frac_timed {r['frac_timed']} "
-              f"kernel_ms {r['kernel_ms_per_launch']} ceiling {bc.get('achieved')} ({bc.get('best_pattern')})")
+              f"{[round(x * 1e3, 1) for x in d['runs_ms']]} frac {r['frac']} (traffic x{r.get('traffic_per_algorithmic')}) "
+              f"launch frac {rl['frac']} kernel_ms {rl['kernel_ms_per_launch']} ceiling {bc.get('achieved')} "
+              f"({bc.get('best_pattern')})")
         if "pmd" in d:
             p = d["pmd"]
             print(f"   pmd steady {p['steady_mpkt_s']:.0f} ({p['steady_frac']}), 1-batch post {p['single_batch_post_to_done_us_median']} us, "
