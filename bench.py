@@ -679,6 +679,83 @@ def roofline_block(res, world, group, args):
     return out
 
 
+def job_cpu_share() -> tuple:
+    """(threads, note): the job's CPU share. The affinity mask of a GPU box
+    lists every core of the host, but the job's share is $OMP_NUM_THREADS
+    (16 on the pool's one-GPU boxes)."""
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    n = max(1, min(affinity, share if share > 0 else affinity))
+    note = (f"the job's CPU share: OMP_NUM_THREADS={share} of {affinity} cores in the affinity mask" if share > 0
+            else f"every core of the affinity mask ({affinity})")
+    return n, note
+
+
+def e2e_leg(args, dev) -> dict:
+    """North star: packets start and end in host memory. The end-to-end rate
+    of cop_process_host_stream over an mbuf-like host pool (NB_MBUF = 131072
+    buffers 2176 bytes apart, data at 128 bytes of headroom, init.h:38-44),
+    visited `passes` times: the host threads gather each batch's 16-byte header
+    records into pinned staging (and copy the previous batch's 8-byte records
+    out), hipMemcpyAsync H2D, the pipeline (stage P + firewall, fw1k), D2H;
+    lanes (HIP streams, not threads) overlap batches. Host threads = the
+    job's CPU share, the caller included (HIP's own runtime threads aside):
+    the count the CPU baseline's multicore leg runs. Checked against the device-resident
+    pipeline's own records for the same packets (no oracle here)."""
+    NB, STRIDE, HEAD = 131072, 2176, 128
+    threads, note = job_cpu_share()
+    fw = cg.gen_rules(0x5EED1002, 1000, cg.GEN_FW, 20)
+    pk = cg.gen_trace(copdist.shard_seed(0x5EED0002, 0, 0), NB, fw)
+    pool = np.zeros(NB * STRIDE, dtype=np.uint8)
+    pool.reshape(NB, STRIDE)[:, HEAD:HEAD + 64] = pk.reshape(NB, 64)
+    passes = 16
+    n = passes * NB
+    ptrs = (pool.ctypes.data + HEAD + (np.arange(n, dtype=np.uint64) % NB) * STRIDE).astype(np.uint64)
+    out = np.zeros(n, dtype=cg.RESULT_DT)
+    res = {"pool": f"{NB} mbufs x {STRIDE} B (headroom {HEAD}), {passes} passes = {n} packets per run",
+           "stages": "parse + firewall (fw1k)", "cores_note": note, "rows": []}
+    want = None
+    best = None
+    rows = [(2, threads, 262144), (4, threads, 262144), (2, threads, 65536), (2, 1, 262144)]
+    for lanes, thr, batch in rows:
+        ctx = cg.Context(device=dev, stages=cg.STAGE_PARSE | cg.STAGE_FW, max_batch=262144, n_streams=lanes)
+        try:
+            ctx.set_fw_table(cg.LpmTable(fw, 1024, 24, True))
+            if want is None:
+                # the device-resident kernel's records for the pool's packets
+                d_p = ctx.alloc(pk.nbytes)
+                d_p.upload(pk)
+                d_r = ctx.alloc(NB * 8)
+                ctx.submit([cg.make_batch(d_p, NB, d_r)])
+                ctx.sync()
+                want = d_r.download(cg.RESULT_DT, NB)
+            ctx.set_host_threads(thr)
+            ctx.process_host_stream(ptrs, batch, out=out)     # warm (pinned staging, pool pages)
+            ok = bool(np.array_equal(out[:NB].view(np.uint8), want.view(np.uint8)) and
+                      np.array_equal(out[-NB:].view(np.uint8), want.view(np.uint8)))
+            times = []
+            for _ in range(7):
+                t0 = time.perf_counter()
+                ctx.process_host_stream(ptrs, batch, out=out)
+                times.append(time.perf_counter() - t0)
+            t = float(np.median(times))
+            row = {"lanes": lanes, "host_threads": thr, "batch": batch, "mpkt_s": round(n / t / 1e6, 3),
+                   "h2d_gb_s": round(n * 16 / t / 1e9, 2), "d2h_gb_s": round(n * 8 / t / 1e9, 2),
+                   "runs_ms": [round(x * 1e3, 3) for x in times], "matches_device_records": ok}
+            res["rows"].append(row)
+            log(f"[rank 0] e2e {row}")
+            if thr == threads and ok and (best is None or row["mpkt_s"] > best["mpkt_s"]):
+                best = row
+        finally:
+            ctx.close()
+    if best:
+        res.update(mpkt_s=best["mpkt_s"], threads=threads, lanes=best["lanes"], batch=best["batch"])
+    one = [r for r in res["rows"] if r["host_threads"] == 1]
+    if one:
+        res["one_thread_mpkt_s"] = one[0]["mpkt_s"]
+    return res
+
+
 def cpu_legs(args, W, fw_rules) -> dict:
     """cpu_baseline (1 pinned core) and cpu_baseline_multicore (the job's CPU
     share): the oracle's restatement of the reference coprocessor() loop
@@ -707,18 +784,13 @@ def cpu_legs(args, W, fw_rules) -> dict:
     }
     log(f"[rank 0] cpu baseline {rate:.1f} Mpkt/s on 1 core ({pk} pkts)")
     # one coprocessor thread per host core of this
-    # job's CPU share. The affinity mask of a GPU box lists every core of
-    # the host, but the job's share is $OMP_NUM_THREADS (16 on the pool's
-    # one-GPU boxes): the leg uses that many, and says so
-    affinity = len(os.sched_getaffinity(0))
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    ncores = max(1, min(affinity, share if share > 0 else affinity))
+    # job's CPU share (job_cpu_share): the leg uses that many, and says so
+    ncores, cores_note = job_cpu_share()
     if ncores > 1:
         rate_m, pk_m, secs_m = orc.coprocessor_bench(trace, ns, ofw, args.cpu_budget / 2, ncores, -1)
         out["cpu_baseline_multicore"] = {
             "value": round(rate_m, 3), "unit": "Mpkt/s", "cores": ncores, "kind": "port", "cpu_model": model,
-            "cores_note": (f"the job's CPU share: OMP_NUM_THREADS={share} of {affinity} cores in the affinity "
-                           f"mask" if share > 0 else f"every core of the affinity mask ({affinity})"),
+            "cores_note": cores_note,
             "sample": (f"{pk_m} packets, {ncores} threads each running the restated coprocessor() loop "
                        f"on its own rings and mbuf pool, {secs_m:.1f} s"),
         }
@@ -770,6 +842,9 @@ def main():
     ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the value is their median")
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip rank 0's end-to-end host-memory leg (mbuf pool -> pinned staging -> H2D -> pipeline "
+                         "-> D2H)")
     ap.add_argument("--no-numa-bind", action="store_true",
                     help="do not move the process onto the CPUs of the GPU's NUMA node")
     ap.add_argument("--quick", action="store_true",
@@ -980,7 +1055,22 @@ def main():
     # every N (north_star: "next to the reference DPDK CPU coprocessor timed
     # on the same box's host cores in the same run")
     if rank == 0 and not args.no_cpu:
+        e2e = None
+        if not args.no_e2e:
+            try:
+                e2e = e2e_leg(args, dev)
+            except Exception as e:  # noqa: BLE001 (a report: never fails the line)
+                e2e = {"error": str(e)[:300]}
         out.update(cpu_legs(args, W, res["fw_rules"]))
+        if e2e is not None:
+            mc = out.get("cpu_baseline_multicore") or {}
+            if "mpkt_s" in e2e and mc.get("cores") == e2e.get("threads"):
+                e2e["cpu_same_threads"] = mc["value"]
+                e2e["ratio_vs_cpu_same_threads"] = round(e2e["mpkt_s"] / mc["value"], 3)
+            if "one_thread_mpkt_s" in e2e and out.get("cpu_baseline"):
+                e2e["ratio_one_thread_vs_cpu_one_core"] = round(e2e["one_thread_mpkt_s"] /
+                                                                out["cpu_baseline"]["value"], 3)
+            out["e2e"] = e2e
     group.barrier()   # the other ranks wait for rank 0's CPU legs
 
     if rank == 0:

@@ -630,10 +630,15 @@ class Context:
     def set_host_threads(self, n: int):
         _check(lib().cop_set_host_threads(self.handle, n), self, "set_host_threads")
 
-    def process_host_stream(self, ptrs: np.ndarray, batch: int) -> np.ndarray:
-        """Streaming end-to-end path over host packet addresses (u64 array)."""
+    def process_host_stream(self, ptrs: np.ndarray, batch: int, out: np.ndarray | None = None) -> np.ndarray:
+        """Streaming end-to-end path over host packet addresses (u64 array).
+        out: a RESULT_DT array of len(ptrs) to fill (timed loops reuse one)."""
         ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
-        res = np.zeros(len(ptrs), dtype=RESULT_DT)
+        if out is not None:
+            assert out.dtype == RESULT_DT and len(out) == len(ptrs) and out.flags.c_contiguous
+            res = out
+        else:
+            res = np.zeros(len(ptrs), dtype=RESULT_DT)
         _check(lib().cop_process_host_stream(self.handle, _ptr(ptrs), len(ptrs), batch, _ptr(res)), self,
                "process_host_stream")
         return res

@@ -453,6 +453,41 @@ __device__ __forceinline__ void load_step(const StepGeom &g, const uint8_t *pk0,
     }
 }
 
+// IMIX (a slab with u32 offsets): the same three cooperative 16-byte loads
+// per lane, at the step's packets' own offsets. Lane l holds the offset of
+// the step's packet l (one coalesced dword load per lane, `off`); load c of
+// lane s reads chunk (64c+s) mod 3 of packet (64c+s)/3, whose offset comes
+// over by ds_bpermute, so gather_step applies unchanged. A wave's load
+// instruction then touches about 22 packets' first lines, three lanes per
+// line, where per-lane loads (a dwordx4 at byte 12 across a 16-byte
+// boundary and a dwordx2 at 28) touch 64 lines per instruction, twice.
+// Packet starts are 16-byte aligned and hold 48 readable bytes
+// (include/cop_gpu.h, cop_batch).
+__device__ __forceinline__ void load_step_imix(const StepGeom &g, const uint8_t *pkts, uint32_t off,
+                                               uint32_t data_off, u32x4 (&v)[3], bool sys = false)
+{
+    uint32_t o[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+        o[c] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(g.lpk[c] << 2), (int)off) + data_off + g.lch[c];
+    if (sys) {
+        const __amdgpu_buffer_rsrc_t rs = sys_rsrc(pkts);
+#pragma unroll
+        for (int c = 0; c < 3; c++) v[c] = ld_sys16(rs, o[c]);
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) v[c] = __builtin_nontemporal_load((const u32x4 *)(pkts + o[c]));
+}
+
+// the offset of the step's packet pb + lane (clamped to `last`)
+__device__ __forceinline__ uint32_t load_off_imix(const uint32_t *offsets, uint32_t pb, int lane, uint32_t last,
+                                                  bool sys = false)
+{
+    const uint32_t ic = min(pb + (uint32_t)lane, last);
+    return sys ? ld_sys4(sys_rsrc(offsets), ic * 4u) : offsets[ic];
+}
+
 // The fields of this lane's packet (bytes 12..15 and 24..35) from the step's
 // loads: source lane s holds chunk k of its packet in load (k - s) mod 3, so
 // each field is one select at the source plus one ds_bpermute.

@@ -115,13 +115,34 @@ __device__ __forceinline__ void pmd_leave(const CopKPmd &P, uint32_t why)
 // slot spent on a doorbell. Leaders also turn the host's stop flag, a
 // look-back timeout or an idle spell (no new post on any ring for
 // idle_ticks) into the exit word.
+// XCD-local relays (COPK_PMD_XRELAY, one ring): each XCD has a doorbell
+// leader of its own (the first of its workers to claim it at the census;
+// the XCD from the XCC_ID hardware register), which raises ITS XCD's relay
+// line with a plain store: the line stays in that XCD's L2, and the XCD's
+// workers poll it with non-temporal loads (L1 bypassed, served by the L2),
+// an L2 round trip instead of the memory-side one of an agent-scope poll of
+// a line another XCD's atomic wrote. Nothing crosses XCDs but the gate
+// (published before any relay, as before), which non-leaders also read every
+// 16th poll with the exit word: a fallback that never leaves a worker
+// waiting for a relay that did not come.
+#ifndef COPK_PMD_XRELAY
+#define COPK_PMD_XRELAY 0
+#endif
+__device__ __forceinline__ __attribute__((unused)) uint32_t xcc_id()
+{
+    // s_getreg_b32 HW_REG_XCC_ID (hwreg 20), bits [3:0]
+    return __builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & 7u;
+}
+
 __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd &P, uint32_t r, uint32_t wr,
-                                                                  unsigned long long b, bool leader)
+                                                                  unsigned long long b, bool leader, int xcc = -1)
 {
     // this worker's copy of the relay (one 128-byte line per group of the
     // ring's workers): a thousand pollers on one line would hammer one
     // memory channel while other workers stream
-    unsigned long long *relay = P.d_posted + ((size_t)r * COPK_PMD_RELAYS + wr % COPK_PMD_RELAYS) * 16;
+    const bool xr = xcc >= 0;   // XCD-local relays: line xcc, raised by this XCD's leader only
+    unsigned long long *relay =
+        P.d_posted + ((size_t)r * COPK_PMD_RELAYS + (xr ? (uint32_t)xcc : wr % COPK_PMD_RELAYS)) * 16;
     unsigned long long *relays = P.d_posted + (size_t)r * COPK_PMD_RELAYS * 16;
     unsigned long long *gate = P.d_gate + (size_t)r * 16;
     const unsigned long long *h_posted = P.h_posted + (size_t)r * 8;
@@ -129,8 +150,10 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
     for (uint32_t spins = 0;; spins++) {
         // every load of a poll is issued before any is used: one round trip
         // per poll, not one per load (a leader's PCIe read overlaps the rest)
-        const unsigned long long hp = ld_u64(relay);
-        const uint32_t ex = ld_agent(&P.d_ctl[0]);
+        const bool far = !xr || leader || (spins & 15u) == 15u;
+        const unsigned long long hp = xr ? __builtin_nontemporal_load(relay) : ld_u64(relay);
+        const uint32_t ex = far ? ld_agent(&P.d_ctl[0]) : 0u;
+        const unsigned long long gx = (xr && far) ? ld_u64(gate) : 0ull;
         unsigned long long h = 0;
         uint32_t stop = 0;
         if (leader) {
@@ -139,6 +162,8 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
             stop = __hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (hp > b) return hp;
+        // (XCD-local relays: the gate's published count, the fallback)
+        if (xr && !(gx >> COPK_PMD_GATE_SHIFT) && (gx & GATE_POSTED) > b) return gx & GATE_POSTED;
         if (ex) {
             if (ex == COPK_PMD_ABORT) return 0;
             // idle or stop: the gate was closed before the exit word was set
@@ -151,7 +176,9 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
         if (leader) {
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
             if (h > hp && (COPK_PMD_NOGATE || gate_publish(gate, h, hp))) {
-                for (int x = 0; x < COPK_PMD_RELAYS; x++) atomicMax(relays + x * 16, h);
+                if (xr) __builtin_nontemporal_store(h, relay);   // this XCD's line, kept in its L2
+                else
+                    for (int x = 0; x < COPK_PMD_RELAYS; x++) atomicMax(relays + x * 16, h);
                 if (P.stamps && r == 0) {   // diagnostic: when each doorbell value was relayed
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2], h);
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2 + 1], now);
@@ -233,8 +260,17 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
     uint32_t *s_door = lc.s_misc + 36;   // [0..1] posted, [2] leave, [3] the batch's packets
     stage_tables<FW, LPM>(p, lc.tb, lane, wave);
 
-    // census: every worker and the doorbell resident, or nobody works
+    // census: every worker and the doorbell resident, or nobody works. With
+    // XCD-local relays (one ring) the first worker of each XCD to claim its
+    // XCD's word in the gate line (words 8..15, zeroed per launch) is that
+    // XCD's doorbell leader
+    int xcc = -1;
+    bool xlead = false;
     if (tid == 0) {
+        if (COPK_PMD_XRELAY && P.n_rings == 1) {
+            xcc = (int)xcc_id();
+            xlead = atomicCAS((unsigned long long *)&P.d_gate[8 + xcc], 0ull, 1ull) == 0ull;
+        }
         atomicAdd(&P.d_ctl[1], 1u);
         uint32_t spins = 0;
         while (ld_agent(&P.d_ctl[1]) < P.n_work && ld_agent(&P.d_ctl[0]) == 0) {
@@ -273,7 +309,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         uint32_t slot = (uint32_t)(b % n_slots);
         const uint32_t qb = G / tpb, rb = G % tpb;
         unsigned long long posted = 0;
-        const bool leader = wr % P.relay_stride == 0;
+        const bool leader = xcc >= 0 ? xlead : wr % P.relay_stride == 0;
         unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
         // the tile's completion, by one lane once every wave's stores
         // (write-through) and counter adds have landed: count it for its
@@ -307,7 +343,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             if (b >= posted) {
                 // wait for batch b to be posted (one lane polls the relay)
                 if (tid == 0) {
-                    const unsigned long long hp = wait_posted(P, r, wr, b, leader);
+                    const unsigned long long hp = wait_posted(P, r, wr, b, leader, xcc);
                     s_door[0] = (uint32_t)hp;
                     s_door[1] = (uint32_t)(hp >> 32);
                     s_door[2] = hp == 0 ? 1u : 0u;
@@ -366,8 +402,8 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                 if (j < ntiles) {
                     const CopKBatch bt = pmd_batch(p, rg, slot, n, ntiles);
                     constexpr int WIN = LPM == COPK_TBL_DIR ? COPK_PMD_WIN_DIR : COPK_PMD_WIN;
-                    if (sysld) tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 1, WIN>(p, lc, bt, j, tid_i, lane_i, wave_i);
-                    else tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 0, WIN>(p, lc, bt, j, tid_i, lane_i, wave_i);
+                    if (sysld) tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 1, WIN, LAY>(p, lc, bt, j, tid_i, lane_i, wave_i);
+                    else tile_steps<FW, LPM, PPT, COPK_PMD_WT != 0, 0, WIN, LAY>(p, lc, bt, j, tid_i, lane_i, wave_i);
                 }
             } else {
                 if (P.test_skip && r == 0 && b == 0 && j + 1 == P.test_skip) {
@@ -422,7 +458,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
     // above the closed gate's count; tickets are claimed in order, so every
     // tile of every batch below the gate was claimed by a worker that serves
     // it. A relaunch zeroes the tickets (ticket 0 = tile 0 of batch seq0r).
-    constexpr bool DYN_OK = PPT <= 2 || (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT) <= 2;
+    constexpr bool DYN_OK = (PPT <= 2 || (COPK_PMD_WIN < PPT ? COPK_PMD_WIN : PPT) <= 2) && LAY == COPK_LAY_COALESCED;
     auto serve_dyn = [&](auto steps_c) {
         // (two tiles' loads live at once: 256- and 512-packet tiles, or
         // 1024-packet tiles with a window of at most two steps in flight,
@@ -445,7 +481,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             unsigned long long *ticket = P.d_ticket + ((size_t)r * COPK_PMD_TK_LANES + xl) * 16;
             uint32_t *s_tk = lc.s_misc + 72;   // the next claimed ticket (lo, hi)
             unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
-            const bool leader = wr % P.relay_stride == 0;
+            const bool leader = xcc >= 0 ? xlead : wr % P.relay_stride == 0;
             unsigned long long posted = 0;
             // lane 0 of wave 0: the pending slot count (issued after a tile's
             // stores drained, its return read one tile later)
@@ -504,7 +540,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                         // count first (it may complete a batch), then wait
                         if (tid == 0) {
                             pend_flush();
-                            const unsigned long long hp = wait_posted(P, r, wr, b, leader);
+                            const unsigned long long hp = wait_posted(P, r, wr, b, leader, xcc);
                             s_door[0] = (uint32_t)hp;
                             s_door[1] = (uint32_t)(hp >> 32);
                             s_door[2] = hp == 0 ? 1u : 0u;

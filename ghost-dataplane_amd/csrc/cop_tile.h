@@ -182,16 +182,32 @@ __device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &
     for (uint32_t q = (uint32_t)tid; q <= nb; q += BLOCK) st_u32<WT>(h.off[q], &p.hit_off[tile * (nb + 1) + q]);
 }
 
+// IMIX header loads: three cooperative 16-byte loads per lane and step at
+// the packets' offsets (load_step_imix), or (0) per-lane loads of bytes
+// 12..27 and 28..35. FW + LPM 100k IMIX at the driver's 20 steps: 36,664 /
+// 36,881 / 37,028 against 31,232 / 33,901 / 31,254 Mpkt/s, the one-shot
+// kernel's frac 0.479-0.482 against 0.449-0.486 (profiles/r06/check4/abx_*)
+#ifndef COPK_IMIX_COOP
+#define COPK_IMIX_COOP 1
+#endif
+// IMIX with the route's DIR-24-8 on the poll-mode step path (tile_steps_v):
+// the offsets, header loads, tbl24 and tbl8 probes of successive steps
+// pipelined (1), or the whole-tile body (0)
+#ifndef COPK_IMIX_STEPS
+#define COPK_IMIX_STEPS 1
+#endif
+
 // Whether a tile can run step by step (tile_steps): segmented lists, no
-// optional feature, coalesced 64-byte slots, the firewall in LDS, and the
-// route in LDS or DIR-24-8 (whose two dependent probes tile_steps_v
+// optional feature, the firewall in LDS, and coalesced 64-byte slots with
+// the route in LDS or DIR-24-8 (whose two dependent probes tile_steps_v
 // pipelines across steps; the trie's and the bucketed form's chains are
-// not).
+// not), or IMIX with a DIR-24-8 route.
 template <int FW, int LPM, int LAY, bool EXT>
 constexpr bool steps_ok()
 {
-    return !EXT && LAY == COPK_LAY_COALESCED && FW != COPK_TBL_DIR && FW != COPK_TBL_BKT && LPM != COPK_TBL_TRIE &&
-           LPM != COPK_TBL_BKT;
+    return !EXT && FW != COPK_TBL_DIR && FW != COPK_TBL_BKT &&
+           ((LAY == COPK_LAY_COALESCED && LPM != COPK_TBL_TRIE && LPM != COPK_TBL_BKT) ||
+            (LAY == COPK_LAY_IMIX && COPK_IMIX_STEPS && LPM == COPK_TBL_DIR));
 }
 
 // One tile of the poll-mode kernel, step by step (tile_body does the same
@@ -315,7 +331,7 @@ __device__ __forceinline__ void steps_load(const CopKBatch &B, uint32_t j, int l
 // steps' loads are system-coherent too (as steps_load's were: a reused or
 // host-memory slot, cop_pmd.hip)
 template <int FW, int LPM, int PPT, bool WT, int SYS = 2, int WIN = COPK_PMD_WIN,
-          bool STAGE_LIST = COPK_PMD_STAGE_LIST>
+          bool STAGE_LIST = COPK_PMD_STAGE_LIST, int LAY = COPK_LAY_COALESCED>
 __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
                                              int tid, int lane, int wave, u32x4 (&v)[win_of<PPT, WIN>()][3],
                                              bool sys_rt = false)
@@ -453,7 +469,56 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
             else if (k == 3) step_prio<3>();
         }
     };
-    if constexpr (LPM != COPK_TBL_DIR) {
+    if constexpr (LAY == COPK_LAY_IMIX) {
+        // IMIX (a slab with u32 offsets): five stages across steps, each
+        // round waiting only for loads the previous round issued. Round k:
+        // step k's headers (landed) are gathered and classified and its
+        // tbl24 probe issued; step k + 1's header loads go out at its
+        // offsets (landed); step k + 2's offsets are loaded; step k - 1's
+        // tbl8 load is issued; step k - 2 is finished and written out. The
+        // prologue loads step 0's offsets, then its headers and step 1's
+        // offsets. (The whole-tile body instead waits for every step's
+        // offsets, then every step's headers, then the probes: four
+        // dependent round trips with nothing else in flight.)
+        static_assert(LPM == COPK_TBL_DIR && FW != COPK_TBL_DIR && FW != COPK_TBL_BKT, "IMIX steps: DIR-24-8 route");
+        struct St {
+            uint32_t w3, src, dst, verdict, port, fwe, lpe;
+            bool valid;
+            T8 t8;
+        };
+        St a{}, b{}, c{};
+        u32x4 h[3];
+        uint32_t off = load_off_imix(B.offsets, base + step_off<PPT>(0, wave), lane, last, sys);
+        load_step_imix(sg, B.pkts, off, B.data_off, h, sys);
+        if (PPT > 1) off = load_off_imix(B.offsets, base + step_off<PPT>(1, wave), lane, last, sys);
+#pragma unroll
+        for (int k = 0; k < PPT + 2; k++) {
+            if (k < PPT) {
+                uint32_t w3[1], w6[1], w7[1], w8[1];
+                prio(k);
+                gather_step(sg, h, w3[0], w6[0], w7[0], w8[0]);
+                uint32_t verdict[1], port[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1];
+                pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2, fwe2);
+                a = St{w3[0], src[0], dst[0], verdict[0], port[0], fwe[0], lpe[0],
+                       base + step_off<PPT>(k, wave) + (uint32_t)lane < B.n && B.n != 0, T8{false, 0ull}};
+                if (k + 1 < PPT) {
+                    load_step_imix(sg, B.pkts, off, B.data_off, h, sys);
+                    if (k + 2 < PPT) off = load_off_imix(B.offsets, base + step_off<PPT>(k + 2, wave), lane, last, sys);
+                }
+            }
+            if (k >= 1 && k <= PPT) b.t8 = tbl8_issue(p.lpm_tbl8, p.lpm_tbl8_packed, b.dst, b.lpe);
+            if (k >= 2) {
+                const uint32_t w3[1] = {c.w3}, src[1] = {c.src}, dst[1] = {c.dst}, lpe2[1] = {0}, fwe2[1] = {0};
+                const bool valid[1] = {c.valid};
+                uint32_t verdict[1] = {c.verdict}, fwe[1] = {c.fwe}, flags[1], rnh[1], ct = 0, cn = 0;
+                uint32_t lpe[1] = {tbl8_finish(p.lpm_tbl8, p.lpm_tbl8_packed, c.dst, c.lpe, c.t8)};
+                pass2<FW, LPM, 1, false>(p, w3, src, dst, valid, fwe, lpe, lpe2, fwe2, verdict, flags, rnh, ct, cn);
+                emit(k - 2, valid[0], verdict[0], flags[0], c.port, rnh[0]);
+            }
+            c = b;
+            b = a;
+        }
+    } else if constexpr (LPM != COPK_TBL_DIR) {
         // LDS-only lookups: each step classified as its headers land
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
@@ -524,15 +589,16 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
     step_prio<3>();
 }
 
-// One tile of the poll-mode kernel, step by step: loads, then tile_steps_v.
-template <int FW, int LPM, int PPT, bool WT, int SYS, int WIN = COPK_PMD_WIN>
+// One tile of the poll-mode kernel, step by step: loads, then tile_steps_v
+// (IMIX: tile_steps_v issues every load itself)
+template <int FW, int LPM, int PPT, bool WT, int SYS, int WIN = COPK_PMD_WIN, int LAY = COPK_LAY_COALESCED>
 __device__ __forceinline__ void tile_steps(const CopKParams &p, const LdsCarve &lc, const CopKBatch &B, uint32_t j,
                                            int tid, int lane, int wave)
 {
     u32x4 v[win_of<PPT, WIN>()][3];
     step_prio<0>();
-    steps_load<PPT, 0, win_of<PPT, WIN>(), SYS, WIN>(B, j, lane, wave, v);
-    tile_steps_v<FW, LPM, PPT, WT, SYS, WIN>(p, lc, B, j, tid, lane, wave, v);
+    if constexpr (LAY != COPK_LAY_IMIX) steps_load<PPT, 0, win_of<PPT, WIN>(), SYS, WIN>(B, j, lane, wave, v);
+    tile_steps_v<FW, LPM, PPT, WT, SYS, WIN, COPK_PMD_STAGE_LIST, LAY>(p, lc, B, j, tid, lane, wave, v);
 }
 
 // One tile of 256 * PPT packets (base = j * TILE) of batch B: header loads,
@@ -584,6 +650,18 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
 #pragma unroll
         for (int k = 0; k < PPT; k++) gather_step(sg, v[k], w3[k], w6[k], w7[k], w8[k]);
 #endif
+    } else if (IMIX && COPK_IMIX_COOP && B.n) {
+        // IMIX: the offsets (coalesced), then three cooperative 16-byte loads
+        // per lane and step at the packets' offsets (load_step_imix)
+        const StepGeom sg = step_geom(lane);
+        uint32_t off[PPT];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) off[k] = load_off_imix(B.offsets, base + k * BLOCK + wave * 64, lane, last, sys);
+        u32x4 v[PPT][3];
+#pragma unroll
+        for (int k = 0; k < PPT; k++) load_step_imix(sg, B.pkts, off[k], B.data_off, v[k], sys);
+#pragma unroll
+        for (int k = 0; k < PPT; k++) gather_step(sg, v[k], w3[k], w6[k], w7[k], w8[k]);
     } else if (LAY == COPK_LAY_HDR16 && B.n) {
         // one 16-byte record per packet: frame bytes 12..15 then 24..35
 #pragma unroll

@@ -278,6 +278,32 @@ def test_process_host_stream_lanes(gpu_ctx_factory, lanes, threads):
     assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
 
 
+@pytest.mark.parametrize("lanes,threads", [(2, 16), (4, 5)])
+def test_process_host_stream_large_batches(gpu_ctx_factory, lanes, threads):
+    """The end-to-end path as bench.py's e2e leg runs it: 256k-packet
+    batches, the records of each lane's previous batch copied out by the host
+    threads in the same job as the next gather (GatherPool::run), a ragged
+    last batch; 3 x 262144 + 77 packets, each of a 50k-packet mbuf pool
+    visited many times, against the oracle."""
+    rules = fw1k()
+    ctx = setup_ctx(gpu_ctx_factory, rules, n_streams=lanes, max_batch=262144)
+    ctx.set_host_threads(threads)
+    nb = 50000
+    pk = cg.gen_trace(0x5EED0710, nb, rules)
+    stride = 2176
+    pool = np.zeros(nb * stride, dtype=np.uint8)
+    pool.reshape(nb, stride)[:, 128:192] = pk.reshape(nb, 64)
+    n = 3 * 262144 + 77
+    sel = np.random.default_rng(5).integers(0, nb, n)
+    ptrs = (pool.ctypes.data + 128 + sel.astype(np.uint64) * stride).astype(np.uint64)
+    fwo, _ = oracle_tables(rules)
+    ro, _, _ = orc.process(pk, nb, stages=S | F, fw=fwo)
+    out = np.full(n, 0xEE, np.uint64).view(cg.RESULT_DT)
+    for _ in range(2):     # the second pass reuses the lanes' staging
+        res = ctx.process_host_stream(ptrs, 262144, out=out)
+        assert np.array_equal(res.view(np.uint8), ro[sel].view(np.uint8))
+
+
 @pytest.mark.parametrize("lanes", [1, 4])
 def test_concurrent_lanes_many_submits(gpu_ctx_factory, lanes):
     """Back-to-back submits spread over lanes (kernels may overlap): every

@@ -361,3 +361,57 @@ def test_pmd_look_back_give_up_completes_nothing(gpu_ctx_factory, monkeypatch):
     c0 = int(np.sum(fos[0] < B // tpb))       # tile 0's forwarded packets
     assert np.array_equal(fwd[:c0], fos[0][:c0])
     assert (fwd[c0:B] == 0xFFFFFFFF).all()
+
+
+@pytest.mark.parametrize("flags", [0, cg.PMD_SYS_ACQUIRE, cg.PMD_STATIC_SLOTS])
+def test_pmd_imix_steps_ragged_and_rewritten(gpu_ctx_factory, flags):
+    """IMIX on the poll-mode step path (segmented lists: offsets, headers,
+    tbl24 and tbl8 of successive steps pipelined, cop_tile.h tile_steps_v):
+    a ragged batch (20,003 packets: a last tile of 547 packets, a last step
+    of 35), slots rewritten between generations (a new slab and new offsets
+    each time, except with COP_PMD_STATIC_SLOTS), read with the plain,
+    coherent-once-wrapped and coherent-every-tile loads; every generation's
+    records and segment lists against the oracle."""
+    from test_gpu_seg import nseg, seg_to_dense
+    rules = fw1k()
+    rts = routes(20000)
+    ctx = gpu_ctx_factory(stages=S | F | L, flags=cg.CFG_SEG_LISTS)
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    ctx.set_route_lpm(cg.LpmTable(rts, 1 << 20, 1 << 16, False))
+    fw, rt = oracle_tables(rules, rts)
+    B, P = 20003, 2
+    gens = [cg.gen_imix(0x5EED0B60 + g, B, rules, rts) for g in range(6)]
+    per = max(((sl.nbytes + of.nbytes + 4095) // 4096) * 4096 for sl, of in gens)
+    dp = ctx.alloc(per * P)
+
+    def put(g, s_):
+        sl, of = gens[g]
+        dp.upload(sl, s_ * per)
+        dp.upload(of, s_ * per + per - of.nbytes)   # offsets at the slot's end (16-byte aligned)
+    for s_ in range(P):
+        put(s_, s_)
+    FS = ((B + 3) // 4) * 4
+    dr = ctx.alloc(B * P * 8)
+    df = ctx.alloc(FS * P * 4)
+    dc = ctx.alloc(P * nseg(B) * 4)
+    offs_at = dp.addr + per - gens[0][1].nbytes
+    assert all(of.nbytes == gens[0][1].nbytes for _, of in gens)
+    ring = cg.make_ring(dp, P, B, dr, per, offsets=offs_at, offsets_slot_words=per // 4,
+                        fwd_idx=df, fwd_slot=FS, fwd_count=dc)
+    n_gen = 6 if flags != cg.PMD_STATIC_SLOTS else P
+    with ctx.pmd_start(ring, flags) as m:
+        assert m.info()["kernel_name"] == "cop_pmd<1, 2, 1, 4, false>"
+        for g in range(n_gen):
+            s_ = g % P
+            if g >= P:
+                put(g, s_)
+            m.post(1)
+            m.wait()
+            sl, of = gens[g]
+            ro, fo, _ = orc.process(sl, B, offsets=of, stages=S | F | L, fw=fw, route=rt)
+            res = dr.download(cg.RESULT_DT, B * P)[s_ * B:(s_ + 1) * B]
+            fwd = df.download(np.uint32, FS * P)[s_ * FS:s_ * FS + B]
+            cnt = dc.download(np.uint32, P * nseg(B))[s_ * nseg(B):(s_ + 1) * nseg(B)]
+            assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"generation {g} records"
+            assert np.array_equal(seg_to_dense(fwd, cnt, B), fo), f"generation {g} list"
+        assert m.info()["launches"] == 1

@@ -73,6 +73,13 @@ for s in "$@"; do
       done
       step 200 "$out/mb_fetch.log" rocprofv3 --pmc FETCH_SIZE -d "$out/mb_fetch" -o mb --output-format csv -- "$R/tools/membench"
       step 200 "$out/mb_write.log" rocprofv3 --pmc WRITE_SIZE -d "$out/mb_write" -o mb --output-format csv -- "$R/tools/membench" ;;
+    pmc_l2)
+      # L2 hits and misses of the poll-mode kernel over exactly K posted
+      # batches, per workload (the probes' L2 miss ratio beside the traffic)
+      for wk in ${PMC_WORKLOADS:-fw1k:1024 fw_lpm:1024}; do
+        w=${wk%%:*}; k=${wk##*:}
+        step 300 "$out/l2_${w}.log" rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$out/l2_${w}" -o l2 --output-format csv -- python3 "$R/tools/pmc_pmd.py" run --workload "$w" --batches "$k"
+      done ;;
     pmc_oneshot)
       # the one-shot kernel's PMC passes over the driver's command (reduce
       # here with tools/pmc_traffic.py and the membench passes of pmc_pmd)
@@ -112,6 +119,17 @@ for s in "$@"; do
       step 300 "$out/tail_main.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
       COP_LIB="$R/ghost-dataplane_amd/libcopgpu_$x.so" step 300 "$out/tail_$x.log" python3 -u "$R/tools/pmd_tail.py" --posts 60
       grep -h "post->done\|slot on CU (w // 256)  [04]" "$out/tail_main.log" "$out/tail_$x.log" ;;
+    abx:*)
+      # an experiment build against the default build on the workload of
+      # $BENCH_ARGS (e.g. --workload fw_lpm_imix), alternating three pairs:
+      # the poll-mode 20-step value and the one-shot kernel's frac (no tails)
+      x=${s#abx:}; i=0
+      for lib in main $x main $x main $x; do
+        i=$((i + 1))
+        L=""; [ "$lib" != main ] && L="$R/ghost-dataplane_amd/libcopgpu_$x.so"
+        COP_LIB=$L step 300 "$out/abx_${lib}_$i.log" $B --steps 20 --warmup 5 --repeats 11 --secondary none --no-cpu --no-rccl-check $BENCH_ARGS
+        grep -h '^{"metric"' "$out/abx_${lib}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); p=d.get("pmd",{}); r=d["roofline"]; rl=d.get("roofline_launch", r); print("abx", sys.argv[1], d["value"], "timed", r["frac_timed"], "probe", r.get("probe_bound"), "launch frac", rl["frac"], "launch probe", rl.get("probe_bound"), "steady", p.get("steady_frac"), "one-batch", p.get("single_batch_post_to_done_us_median"))' "$lib"
+      done ;;
     envab:*)
       # an environment setting (envab:NAME=VALUE) against the default on the
       # driver's command, alternating three pairs, then the poll-mode,
