@@ -78,10 +78,13 @@ struct Lane {
     hipEvent_t ev[TIMING_SLOTS][2];
     int ev_head = 0, ev_count = 0, ev_created = 0;
     hipEvent_t join = nullptr;                      // timer joins
-    // streaming host-path slot
-    uint8_t *h_stage = nullptr, *d_stage = nullptr;
-    cop_result *h_res = nullptr, *d_res = nullptr;
+    // streaming host-path slot (zc: staging and records in mapped pinned
+    // memory, m_* their device addresses; the kernel reads and writes them
+    // over PCIe, no copy-engine transfers)
+    uint8_t *h_stage = nullptr, *d_stage = nullptr, *m_stage = nullptr;
+    cop_result *h_res = nullptr, *d_res = nullptr, *m_res = nullptr;
     uint32_t cap = 0;
+    bool zc = false;
     hipEvent_t done = nullptr;
     bool busy = false;
     uint64_t first = 0;
@@ -261,6 +264,10 @@ struct cop_ctx {
     // the header records from, and writes its records to, mapped pinned host
     // memory (no copy-engine round trips); up to zc_max packets ($COP_ZC_MAX)
     uint32_t zc_max = 65536;
+    // cop_process_host_stream: staging and records in mapped pinned memory,
+    // read and written by the kernel over PCIe ($COP_STREAM_ZC=1), or copied
+    // by the copy engines (0)
+    bool stream_zc = false;
     uint8_t *zc_stage = nullptr;      // mapped pinned: records in
     cop_result *zc_res = nullptr;     // mapped pinned: results out
     uint32_t *zc_fwd = nullptr;       // mapped pinned: forward list + count
@@ -552,6 +559,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_DBG")) c->dbg = (uint32_t)strtoul(e, nullptr, 0);
     if (const char *e = getenv("COP_LDS_PAD")) c->lds_pad = (uint32_t)strtoul(e, nullptr, 0) & ~15u;
     if (const char *e = getenv("COP_ZC_MAX")) c->zc_max = (uint32_t)strtoul(e, nullptr, 0);
+    if (const char *e = getenv("COP_STREAM_ZC")) c->stream_zc = atoi(e) != 0;
     if (const char *e = getenv("COP_LOADS")) c->coalesced = strcmp(e, "strided") != 0;
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
     if (const char *e = getenv("COP_HIT_BINS")) c->hit_bins = atoi(e) != 0;
@@ -1555,20 +1563,32 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
     if (!c || (n && (!pkt_data || !results)) || batch == 0) return -EINVAL;
     if (batch > c->cfg.max_batch) return set_err(c, -EINVAL, "batch %u > max_batch", batch);
     if (int rc = sync_lanes(c)) return rc;
+    const bool zc = c->stream_zc;
     for (int l = 0; l < c->n_lanes; l++) {
         Lane &L = c->lane[l];
-        if (L.cap >= batch) continue;
+        if (L.cap >= batch && L.zc == zc) continue;
         if (L.h_stage) (void)hipHostFree(L.h_stage);
         if (L.h_res) (void)hipHostFree(L.h_res);
         if (L.d_stage) (void)hipFree(L.d_stage);
         if (L.d_res) (void)hipFree(L.d_res);
-        L.h_stage = L.d_stage = nullptr;
-        L.h_res = L.d_res = nullptr;
+        L.h_stage = L.d_stage = L.m_stage = nullptr;
+        L.h_res = L.d_res = L.m_res = nullptr;
         L.cap = 0;
-        HIPCHK(c, hipHostMalloc(&L.h_stage, (size_t)batch * COP_HDR16_STRIDE, hipHostMallocDefault));
-        HIPCHK(c, hipHostMalloc(&L.h_res, (size_t)batch * 8, hipHostMallocDefault));
-        HIPCHK(c, hipMalloc(&L.d_stage, (size_t)batch * COP_HDR16_STRIDE));
-        HIPCHK(c, hipMalloc(&L.d_res, (size_t)batch * 8));
+        L.zc = zc;
+        if (zc) {
+            HIPCHK(c, hipHostMalloc(&L.h_stage, (size_t)batch * COP_HDR16_STRIDE, hipHostMallocMapped));
+            HIPCHK(c, hipHostMalloc(&L.h_res, (size_t)batch * 8, hipHostMallocMapped));
+            void *ds = nullptr, *dr = nullptr;
+            HIPCHK(c, hipHostGetDevicePointer(&ds, L.h_stage, 0));
+            HIPCHK(c, hipHostGetDevicePointer(&dr, L.h_res, 0));
+            L.m_stage = (uint8_t *)ds;
+            L.m_res = (cop_result *)dr;
+        } else {
+            HIPCHK(c, hipHostMalloc(&L.h_stage, (size_t)batch * COP_HDR16_STRIDE, hipHostMallocDefault));
+            HIPCHK(c, hipHostMalloc(&L.h_res, (size_t)batch * 8, hipHostMallocDefault));
+            HIPCHK(c, hipMalloc(&L.d_stage, (size_t)batch * COP_HDR16_STRIDE));
+            HIPCHK(c, hipMalloc(&L.d_res, (size_t)batch * 8));
+        }
         L.cap = batch;
     }
     int lane = 0;
@@ -1594,15 +1614,16 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
             if (prev_n) memcpy(results + L.first, prev, (size_t)prev_n * sizeof(cop_result));
             host_gather(c, pkt_data + first, L.h_stage, k);
         }
-        HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * COP_HDR16_STRIDE, hipMemcpyHostToDevice, L.s));
+        if (!zc)
+            HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * COP_HDR16_STRIDE, hipMemcpyHostToDevice, L.s));
         cop_batch b;
         memset(&b, 0, sizeof(b));
-        b.pkts = L.d_stage;
+        b.pkts = zc ? L.m_stage : L.d_stage;
         b.n = k;
         b.stride = COP_HDR16_STRIDE;
-        b.results = L.d_res;
+        b.results = zc ? L.m_res : L.d_res;
         if (int rc = submit_on(c, L, &b, 1, false, c->cfg.stages)) return rc;
-        HIPCHK(c, hipMemcpyAsync(L.h_res, L.d_res, (size_t)k * 8, hipMemcpyDeviceToHost, L.s));
+        if (!zc) HIPCHK(c, hipMemcpyAsync(L.h_res, L.d_res, (size_t)k * 8, hipMemcpyDeviceToHost, L.s));
         HIPCHK(c, hipEventRecord(L.done, L.s));
         L.busy = true;
         L.first = first;

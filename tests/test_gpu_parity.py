@@ -278,13 +278,16 @@ def test_process_host_stream_lanes(gpu_ctx_factory, lanes, threads):
     assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
 
 
-@pytest.mark.parametrize("lanes,threads", [(2, 16), (4, 5)])
-def test_process_host_stream_large_batches(gpu_ctx_factory, lanes, threads):
+@pytest.mark.parametrize("lanes,threads,zc", [(2, 16, 0), (4, 5, 0), (2, 16, 1), (3, 1, 1)])
+def test_process_host_stream_large_batches(gpu_ctx_factory, monkeypatch, lanes, threads, zc):
     """The end-to-end path as bench.py's e2e leg runs it: 256k-packet
     batches, the records of each lane's previous batch copied out by the host
     threads in the same job as the next gather (GatherPool::run), a ragged
     last batch; 3 x 262144 + 77 packets, each of a 50k-packet mbuf pool
-    visited many times, against the oracle."""
+    visited many times, against the oracle. zc: staging and records in
+    mapped pinned memory, read and written by the kernel over PCIe
+    ($COP_STREAM_ZC, no copy-engine transfers)."""
+    monkeypatch.setenv("COP_STREAM_ZC", str(zc))
     rules = fw1k()
     ctx = setup_ctx(gpu_ctx_factory, rules, n_streams=lanes, max_batch=262144)
     ctx.set_host_threads(threads)
