@@ -84,7 +84,7 @@ struct Lane {
     uint8_t *h_stage = nullptr, *d_stage = nullptr, *m_stage = nullptr;
     cop_result *h_res = nullptr, *d_res = nullptr, *m_res = nullptr;
     uint32_t cap = 0;
-    bool zc = false;
+    int zc = -1;   // the COP_STREAM_ZC mode the slot was allocated for
     hipEvent_t done = nullptr;
     bool busy = false;
     uint64_t first = 0;
@@ -264,10 +264,13 @@ struct cop_ctx {
     // the header records from, and writes its records to, mapped pinned host
     // memory (no copy-engine round trips); up to zc_max packets ($COP_ZC_MAX)
     uint32_t zc_max = 65536;
-    // cop_process_host_stream: staging and records in mapped pinned memory,
-    // read and written by the kernel over PCIe ($COP_STREAM_ZC=1), or copied
-    // by the copy engines (0)
-    bool stream_zc = false;
+    // cop_process_host_stream: the staged records copied H2D by the copy
+    // engine and the result records written by the kernel straight into
+    // mapped pinned memory (2, the default: the copy engine, which
+    // serialises a lane's H2D and D2H copies, moves 16 bytes per packet
+    // instead of 24), staging and records both mapped and moved by the
+    // kernel over PCIe (1), or both copied (0); $COP_STREAM_ZC
+    int stream_zc = 2;
     uint8_t *zc_stage = nullptr;      // mapped pinned: records in
     cop_result *zc_res = nullptr;     // mapped pinned: results out
     uint32_t *zc_fwd = nullptr;       // mapped pinned: forward list + count
@@ -559,7 +562,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_DBG")) c->dbg = (uint32_t)strtoul(e, nullptr, 0);
     if (const char *e = getenv("COP_LDS_PAD")) c->lds_pad = (uint32_t)strtoul(e, nullptr, 0) & ~15u;
     if (const char *e = getenv("COP_ZC_MAX")) c->zc_max = (uint32_t)strtoul(e, nullptr, 0);
-    if (const char *e = getenv("COP_STREAM_ZC")) c->stream_zc = atoi(e) != 0;
+    if (const char *e = getenv("COP_STREAM_ZC")) c->stream_zc = std::min(2, std::max(0, atoi(e)));
     if (const char *e = getenv("COP_LOADS")) c->coalesced = strcmp(e, "strided") != 0;
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
     if (const char *e = getenv("COP_HIT_BINS")) c->hit_bins = atoi(e) != 0;
@@ -1563,7 +1566,9 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
     if (!c || (n && (!pkt_data || !results)) || batch == 0) return -EINVAL;
     if (batch > c->cfg.max_batch) return set_err(c, -EINVAL, "batch %u > max_batch", batch);
     if (int rc = sync_lanes(c)) return rc;
-    const bool zc = c->stream_zc;
+    // zc 1: staging and records mapped; 2: records mapped, staging copied
+    const int zc = c->stream_zc;
+    const bool zc_in = zc == 1, zc_out = zc != 0;
     for (int l = 0; l < c->n_lanes; l++) {
         Lane &L = c->lane[l];
         if (L.cap >= batch && L.zc == zc) continue;
@@ -1575,18 +1580,22 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
         L.h_res = L.d_res = L.m_res = nullptr;
         L.cap = 0;
         L.zc = zc;
-        if (zc) {
+        if (zc_in) {
             HIPCHK(c, hipHostMalloc(&L.h_stage, (size_t)batch * COP_HDR16_STRIDE, hipHostMallocMapped));
-            HIPCHK(c, hipHostMalloc(&L.h_res, (size_t)batch * 8, hipHostMallocMapped));
-            void *ds = nullptr, *dr = nullptr;
+            void *ds = nullptr;
             HIPCHK(c, hipHostGetDevicePointer(&ds, L.h_stage, 0));
-            HIPCHK(c, hipHostGetDevicePointer(&dr, L.h_res, 0));
             L.m_stage = (uint8_t *)ds;
-            L.m_res = (cop_result *)dr;
         } else {
             HIPCHK(c, hipHostMalloc(&L.h_stage, (size_t)batch * COP_HDR16_STRIDE, hipHostMallocDefault));
-            HIPCHK(c, hipHostMalloc(&L.h_res, (size_t)batch * 8, hipHostMallocDefault));
             HIPCHK(c, hipMalloc(&L.d_stage, (size_t)batch * COP_HDR16_STRIDE));
+        }
+        if (zc_out) {
+            HIPCHK(c, hipHostMalloc(&L.h_res, (size_t)batch * 8, hipHostMallocMapped));
+            void *dr = nullptr;
+            HIPCHK(c, hipHostGetDevicePointer(&dr, L.h_res, 0));
+            L.m_res = (cop_result *)dr;
+        } else {
+            HIPCHK(c, hipHostMalloc(&L.h_res, (size_t)batch * 8, hipHostMallocDefault));
             HIPCHK(c, hipMalloc(&L.d_res, (size_t)batch * 8));
         }
         L.cap = batch;
@@ -1614,16 +1623,16 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
             if (prev_n) memcpy(results + L.first, prev, (size_t)prev_n * sizeof(cop_result));
             host_gather(c, pkt_data + first, L.h_stage, k);
         }
-        if (!zc)
+        if (!zc_in)
             HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * COP_HDR16_STRIDE, hipMemcpyHostToDevice, L.s));
         cop_batch b;
         memset(&b, 0, sizeof(b));
-        b.pkts = zc ? L.m_stage : L.d_stage;
+        b.pkts = zc_in ? L.m_stage : L.d_stage;
         b.n = k;
         b.stride = COP_HDR16_STRIDE;
-        b.results = zc ? L.m_res : L.d_res;
+        b.results = zc_out ? L.m_res : L.d_res;
         if (int rc = submit_on(c, L, &b, 1, false, c->cfg.stages)) return rc;
-        if (!zc) HIPCHK(c, hipMemcpyAsync(L.h_res, L.d_res, (size_t)k * 8, hipMemcpyDeviceToHost, L.s));
+        if (!zc_out) HIPCHK(c, hipMemcpyAsync(L.h_res, L.d_res, (size_t)k * 8, hipMemcpyDeviceToHost, L.s));
         HIPCHK(c, hipEventRecord(L.done, L.s));
         L.busy = true;
         L.first = first;

@@ -278,7 +278,7 @@ def test_process_host_stream_lanes(gpu_ctx_factory, lanes, threads):
     assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
 
 
-@pytest.mark.parametrize("lanes,threads,zc", [(2, 16, 0), (4, 5, 0), (2, 16, 1), (3, 1, 1)])
+@pytest.mark.parametrize("lanes,threads,zc", [(2, 16, 0), (4, 5, 0), (2, 16, 1), (3, 1, 1), (4, 16, 2), (1, 3, 2)])
 def test_process_host_stream_large_batches(gpu_ctx_factory, monkeypatch, lanes, threads, zc):
     """The end-to-end path as bench.py's e2e leg runs it: 256k-packet
     batches, the records of each lane's previous batch copied out by the host

@@ -5,9 +5,11 @@ mbuf-like host pool (NB_MBUF = 131072 buffers at 2176 B stride, data at
 128 B headroom, init.h:38-44); cop_process_host_stream packs each batch's
 16-byte header records (COP_HDR16_STRIDE: frame bytes 12..15, 24..35) into
 pinned staging, copies H2D, runs the pipeline,
-copies the 8-byte records D2H, with the lanes overlapping; the gather runs
-on 1..16 host threads (cop_set_host_threads). Results of the first pool
-pass are checked bit-exactly against the oracle.
+copies the 8-byte records D2H, with the lanes overlapping (or, zc, the
+kernel reads and writes mapped pinned memory: $COP_STREAM_ZC); the gather
+runs on 1..16 host threads (cop_set_host_threads), never more than the
+job's CPU share. Results of the first pool pass are checked bit-exactly
+against the oracle.
 """
 import os
 import sys
@@ -29,42 +31,66 @@ def main():
     pool = np.zeros(NB_MBUF * STRIDE, dtype=np.uint8)
     pool.reshape(NB_MBUF, STRIDE)[:, HEADROOM:HEADROOM + 64] = pk.reshape(NB_MBUF, 64)
     base = pool.ctypes.data + HEADROOM
-    n = 16 * NB_MBUF
+    n = 64 * NB_MBUF
     ptrs = (base + (np.arange(n, dtype=np.uint64) % NB_MBUF) * STRIDE).astype(np.uint64)
+    out = np.zeros(n, dtype=cg.RESULT_DT)
 
     import oracle as orc
     o = orc.OracleLpm(1024, 24)
     o.setup(fw["ip"], fw["depth"], fw["next_hop"])
     ro, _, _ = orc.process(pk, NB_MBUF, stages=3, fw=o)
 
-    print(f"{'lanes':>5s} {'thr':>3s} {'batch':>7s} {'Mpkt/s':>9s} {'GB/s H2D':>9s}  parity")
-    for lanes, threads in ((1, 1), (2, 1), (4, 1), (2, 4), (4, 4), (2, 8), (4, 8), (2, 16), (4, 16)):
-        ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=lanes)
-        ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
-        ctx.set_host_threads(threads)
-        for batch in (16384, 65536, 262144):
-            res = ctx.process_host_stream(ptrs[:NB_MBUF], batch)    # warm + parity
-            ok = np.array_equal(res.view(np.uint8), ro.view(np.uint8))
-            t0 = time.perf_counter()
-            res = ctx.process_host_stream(ptrs, batch)
-            dt = time.perf_counter() - t0
-            print(f"{lanes:5d} {threads:3d} {batch:7d} {n / dt / 1e6:9.1f} {n * cg.HDR16_STRIDE / dt / 1e9:9.2f}  "
-                  f"{'ok' if ok else 'MISMATCH'}", flush=True)
-        ctx.close()
-    # synchronous single-batch path (cop_process_host) for reference
+    # host threads never above the job's CPU share ($OMP_NUM_THREADS, 16 on
+    # the pool's one-GPU boxes): more gather threads than cores collapse
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    print(f"{'lanes':>5s} {'thr':>3s} {'zc':>2s} {'batch':>7s} {'Mpkt/s':>9s} {'GB/s H2D':>9s}  parity", flush=True)
+    for zc in (0, 1, 2):
+        os.environ["COP_STREAM_ZC"] = str(zc)
+        for lanes in (2, 4):
+            for threads in (1, 2, 4, 8, 12, 16):
+                if threads > share:
+                    continue
+                ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=lanes, max_batch=262144)
+                ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
+                ctx.set_host_threads(threads)
+                batch = 262144
+                res = ctx.process_host_stream(ptrs[:NB_MBUF], batch)    # warm + parity
+                ok = np.array_equal(res.view(np.uint8), ro.view(np.uint8))
+                ts = []
+                for _ in range(5):
+                    t0 = time.perf_counter()
+                    ctx.process_host_stream(ptrs, batch, out=out)
+                    ts.append(time.perf_counter() - t0)
+                dt = float(np.median(ts))
+                print(f"{lanes:5d} {threads:3d} {zc:2d} {batch:7d} {n / dt / 1e6:9.1f} {n * cg.HDR16_STRIDE / dt / 1e9:9.2f}  "
+                      f"{'ok' if ok else 'MISMATCH'}", flush=True)
+                ctx.close()
+    os.environ.pop("COP_STREAM_ZC", None)
+    # the H2D copy alone: pinned staging -> HBM, 4 MiB chunks, the copy engine's rate
     ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW)
-    ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
-    res, fwd = ctx.process_host(pk, 65536)
-    t0 = time.perf_counter()
-    for _ in range(8):
-        ctx.process_host(pk, 65536)
-    dt = time.perf_counter() - t0
-    print(f"cop_process_host (sync, 64k, incl. Python pointer list): {8 * 65536 / dt / 1e6:.1f} Mpkt/s")
+    lib = cg.lib()
+    import ctypes
+    hp = ctypes.c_void_p()
+    nbytes = 64 << 20
+    if lib.cop_host_alloc_pinned(ctx.handle, nbytes, ctypes.byref(hp)) == 0:
+        d = ctx.alloc(nbytes)
+        f = lib.cop_memcpy_h2d
+        t0 = time.perf_counter()
+        reps = 20
+        for _ in range(reps):
+            f(ctx.handle, ctypes.c_void_p(d.addr), hp, ctypes.c_uint64(nbytes))
+        ctx.sync()
+        dt = time.perf_counter() - t0
+        print(f"pinned H2D copy, {nbytes >> 20} MiB x {reps}: {reps * nbytes / dt / 1e9:.1f} GB/s", flush=True)
+        lib.cop_host_free_pinned(ctx.handle, hp)
+    ctx.close()
     # the CPU baseline on the same box, same run, per core count: the oracle's
     # restatement of the reference's coprocessor() loop (bench.py's
     # cpu_baseline), so the host paths above read per core against it
     trace = cg.gen_trace(0x5EED0001, NB_MBUF, fw, None)
     for cores in (1, 4, 8, 16):
+        if cores > share:
+            continue
         rate, pk_n, secs = orc.coprocessor_bench(trace, NB_MBUF, o, 3.0, cores, max(os.sched_getaffinity(0)) if cores == 1
                                                  else -1)
         print(f"cpu baseline: restated coprocessor() loop, {cores:2d} thread(s): {rate:9.1f} Mpkt/s "
