@@ -716,8 +716,8 @@ def e2e_leg(args, dev) -> dict:
            "stages": "parse + firewall (fw1k)", "cores_note": note, "rows": []}
     want = None
     best = None
-    rows = [(4, threads, 262144, 2), (2, threads, 262144, 2), (4, threads, 65536, 2), (4, threads, 262144, 0),
-            (4, threads, 262144, 1), (4, 1, 262144, 2)]
+    rows = [(4, threads, 131072, 2), (4, threads, 262144, 2), (4, threads, 65536, 2), (2, threads, 131072, 2),
+            (4, threads, 131072, 0), (4, threads, 131072, 1), (4, 1, 131072, 2)]
     zc0 = os.environ.get("COP_STREAM_ZC")
     for lanes, thr, batch, zc in rows:
         # zc ($COP_STREAM_ZC): 2 (the default) the copy engine moves the

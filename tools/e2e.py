@@ -44,16 +44,16 @@ def main():
     # the pool's one-GPU boxes): more gather threads than cores collapse
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
     print(f"{'lanes':>5s} {'thr':>3s} {'zc':>2s} {'batch':>7s} {'Mpkt/s':>9s} {'GB/s H2D':>9s}  parity", flush=True)
-    for zc in (0, 1, 2):
+    for zc in (int(x) for x in os.environ.get("E2E_MODES", "0,1,2").split(",")):
         os.environ["COP_STREAM_ZC"] = str(zc)
         for lanes in (2, 4):
             for threads in (1, 2, 4, 8, 12, 16):
                 if threads > share:
                     continue
-                ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=lanes, max_batch=262144)
+                batch = 262144
+                ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=lanes, max_batch=batch)
                 ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
                 ctx.set_host_threads(threads)
-                batch = 262144
                 res = ctx.process_host_stream(ptrs[:NB_MBUF], batch)    # warm + parity
                 ok = np.array_equal(res.view(np.uint8), ro.view(np.uint8))
                 ts = []
@@ -65,6 +65,24 @@ def main():
                 print(f"{lanes:5d} {threads:3d} {zc:2d} {batch:7d} {n / dt / 1e6:9.1f} {n * cg.HDR16_STRIDE / dt / 1e9:9.2f}  "
                       f"{'ok' if ok else 'MISMATCH'}", flush=True)
                 ctx.close()
+    # batch size at the default mode (larger copies, fewer per-batch calls)
+    os.environ["COP_STREAM_ZC"] = "2"
+    for lanes, threads, batch in ((4, share, 524288), (4, share, 131072), (4, share, 65536), (3, share, 131072),
+                                  (4, 8, 131072), (4, 4, 131072)):
+        ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=lanes, max_batch=batch)
+        ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
+        ctx.set_host_threads(threads)
+        res = ctx.process_host_stream(ptrs[:NB_MBUF], batch)
+        ok = np.array_equal(res.view(np.uint8), ro.view(np.uint8))
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            ctx.process_host_stream(ptrs, batch, out=out)
+            ts.append(time.perf_counter() - t0)
+        dt = float(np.median(ts))
+        print(f"{lanes:5d} {threads:3d}  2 {batch:7d} {n / dt / 1e6:9.1f} {n * cg.HDR16_STRIDE / dt / 1e9:9.2f}  "
+              f"{'ok' if ok else 'MISMATCH'}", flush=True)
+        ctx.close()
     os.environ.pop("COP_STREAM_ZC", None)
     # the H2D copy alone: pinned staging -> HBM, 4 MiB chunks, the copy engine's rate
     ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW)
