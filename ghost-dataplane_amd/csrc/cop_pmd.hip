@@ -125,6 +125,11 @@ __device__ __forceinline__ void pmd_leave(const CopKPmd &P, uint32_t why)
 // (published before any relay, as before), which non-leaders also read every
 // 16th poll with the exit word: a fallback that never leaves a worker
 // waiting for a relay that did not come.
+// COPK_PMD_XRELAY=2, a fan-out instead: the leaders and relays stay as
+// they are, and the first worker of an XCD whose agent-scope poll sees a new
+// relay value raises an XCD-local line (a workgroup-scope atomic max, done
+// in that XCD's L2), which the XCD's other workers poll with non-temporal
+// loads; each worker's own agent-scope poll runs every fourth poll.
 #ifndef COPK_PMD_XRELAY
 #define COPK_PMD_XRELAY 0
 #endif
@@ -140,9 +145,12 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
     // this worker's copy of the relay (one 128-byte line per group of the
     // ring's workers): a thousand pollers on one line would hammer one
     // memory channel while other workers stream
-    const bool xr = xcc >= 0;   // XCD-local relays: line xcc, raised by this XCD's leader only
+    const bool xr = xcc >= 0 && COPK_PMD_XRELAY == 1;   // XCD-local relays: line xcc, raised by this XCD's leader only
+    const bool xf = xcc >= 0 && COPK_PMD_XRELAY == 2;   // fan-out: XCD-local copies of the relays (one ring)
     unsigned long long *relay =
         P.d_posted + ((size_t)r * COPK_PMD_RELAYS + (xr ? (uint32_t)xcc : wr % COPK_PMD_RELAYS)) * 16;
+    // (fan-out: ring 1's relay lines, unused with one ring)
+    unsigned long long *xline = xf ? P.d_posted + ((size_t)COPK_PMD_RELAYS + (uint32_t)xcc) * 16 : nullptr;
     unsigned long long *relays = P.d_posted + (size_t)r * COPK_PMD_RELAYS * 16;
     unsigned long long *gate = P.d_gate + (size_t)r * 16;
     const unsigned long long *h_posted = P.h_posted + (size_t)r * 8;
@@ -150,8 +158,9 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
     for (uint32_t spins = 0;; spins++) {
         // every load of a poll is issued before any is used: one round trip
         // per poll, not one per load (a leader's PCIe read overlaps the rest)
-        const bool far = !xr || leader || (spins & 15u) == 15u;
-        const unsigned long long hp = xr ? __builtin_nontemporal_load(relay) : ld_u64(relay);
+        const bool far = xf ? (leader || (spins & 3u) == 3u) : (!xr || leader || (spins & 15u) == 15u);
+        const unsigned long long hl = xf ? __builtin_nontemporal_load(xline) : 0ull;
+        const unsigned long long hp = xr ? __builtin_nontemporal_load(relay) : (!xf || far) ? ld_u64(relay) : 0ull;
         const uint32_t ex = far ? ld_agent(&P.d_ctl[0]) : 0u;
         const unsigned long long gx = (xr && far) ? ld_u64(gate) : 0ull;
         unsigned long long h = 0;
@@ -161,7 +170,11 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
             h = __hip_atomic_load(h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             stop = __hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        if (hp > b) return hp;
+        if (xf && hl > b) return hl;
+        if (hp > b) {
+            if (xf) __hip_atomic_fetch_max(xline, hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return hp;
+        }
         // (XCD-local relays: the gate's published count, the fallback)
         if (xr && !(gx >> COPK_PMD_GATE_SHIFT) && (gx & GATE_POSTED) > b) return gx & GATE_POSTED;
         if (ex) {
@@ -179,6 +192,7 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
                 if (xr) __builtin_nontemporal_store(h, relay);   // this XCD's line, kept in its L2
                 else
                     for (int x = 0; x < COPK_PMD_RELAYS; x++) atomicMax(relays + x * 16, h);
+                if (xf) __hip_atomic_fetch_max(xline, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (P.stamps && r == 0) {   // diagnostic: when each doorbell value was relayed
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2], h);
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2 + 1], now);
@@ -269,7 +283,8 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
     if (tid == 0) {
         if (COPK_PMD_XRELAY && P.n_rings == 1) {
             xcc = (int)xcc_id();
-            xlead = atomicCAS((unsigned long long *)&P.d_gate[8 + xcc], 0ull, 1ull) == 0ull;
+            if (COPK_PMD_XRELAY == 1)
+                xlead = atomicCAS((unsigned long long *)&P.d_gate[8 + xcc], 0ull, 1ull) == 0ull;
         }
         atomicAdd(&P.d_ctl[1], 1u);
         uint32_t spins = 0;
@@ -309,7 +324,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         uint32_t slot = (uint32_t)(b % n_slots);
         const uint32_t qb = G / tpb, rb = G % tpb;
         unsigned long long posted = 0;
-        const bool leader = xcc >= 0 ? xlead : wr % P.relay_stride == 0;
+        const bool leader = (xcc >= 0 && COPK_PMD_XRELAY == 1) ? xlead : wr % P.relay_stride == 0;
         unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
         // the tile's completion, by one lane once every wave's stores
         // (write-through) and counter adds have landed: count it for its
@@ -481,7 +496,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             unsigned long long *ticket = P.d_ticket + ((size_t)r * COPK_PMD_TK_LANES + xl) * 16;
             uint32_t *s_tk = lc.s_misc + 72;   // the next claimed ticket (lo, hi)
             unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
-            const bool leader = xcc >= 0 ? xlead : wr % P.relay_stride == 0;
+            const bool leader = (xcc >= 0 && COPK_PMD_XRELAY == 1) ? xlead : wr % P.relay_stride == 0;
             unsigned long long posted = 0;
             // lane 0 of wave 0: the pending slot count (issued after a tile's
             // stores drained, its return read one tile later)

@@ -1623,7 +1623,8 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
             if (prev_n) memcpy(results + L.first, prev, (size_t)prev_n * sizeof(cop_result));
             host_gather(c, pkt_data + first, L.h_stage, k);
         }
-        if (!zc_in)
+        // (c->dbg & 0x100: timing ablation, the H2D copy skipped; results wrong)
+        if (!zc_in && !(c->dbg & 0x100u))
             HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * COP_HDR16_STRIDE, hipMemcpyHostToDevice, L.s));
         cop_batch b;
         memset(&b, 0, sizeof(b));

@@ -83,6 +83,24 @@ def main():
         print(f"{lanes:5d} {threads:3d}  2 {batch:7d} {n / dt / 1e6:9.1f} {n * cg.HDR16_STRIDE / dt / 1e9:9.2f}  "
               f"{'ok' if ok else 'MISMATCH'}", flush=True)
         ctx.close()
+    # timing ablations at the default mode: no H2D copy ($COP_DBG 0x100;
+    # results wrong), and no gather (the same 131072 records every batch)
+    for what, env in (("no H2D copy", {"COP_DBG": "0x100"}),):
+        os.environ.update(env)
+        ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=4, max_batch=131072)
+        ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
+        ctx.set_host_threads(share)
+        ctx.process_host_stream(ptrs[:NB_MBUF], 131072)
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            ctx.process_host_stream(ptrs, 131072, out=out)
+            ts.append(time.perf_counter() - t0)
+        print(f"ablation ({what}), 4 lanes, {share} threads, 131072: {n / float(np.median(ts)) / 1e6:.1f} Mpkt/s",
+              flush=True)
+        ctx.close()
+        for k in env:
+            os.environ.pop(k, None)
     os.environ.pop("COP_STREAM_ZC", None)
     # the H2D copy alone: pinned staging -> HBM, 4 MiB chunks, the copy engine's rate
     ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW)
