@@ -774,12 +774,65 @@ __device__ __forceinline__ void bkt_step(const uint32_t *pairs, const uint32_t (
     }
 }
 
+// The bucketed form's second round split for the poll-mode step pipeline
+// (cop_tile.h tile_steps_v): one packet per lane, its eight pairs' loads
+// issued in one round (bkt_pairs_issue) and used in the next
+// (bkt_pairs_finish: the selection of bkt_step, then its wide-bucket rounds,
+// a wave-uniform loop).
+struct BkQ {
+    u32x4a q[4];
+};
+__device__ __forceinline__ BkQ bkt_pairs_issue(const uint32_t *pairs, uint32_t k0, bool live)
+{
+    BkQ b;
+    if (live) {
+        const uint32_t *a = pairs + 2 * (size_t)k0;
+#pragma unroll
+        for (int h = 0; h < 4; h++) b.q[h] = *(const u32x4a *)(a + 4 * h);
+    } else {
+#pragma unroll
+        for (int h = 0; h < 4; h++) b.q[h] = u32x4a{0u, 0u, 0u, 0u};
+    }
+    return b;
+}
+__device__ __forceinline__ uint32_t bkt_pairs_finish(const uint32_t *pairs, uint32_t ip, uint32_t k0, uint32_t k1,
+                                                     bool live, const BkQ &b)
+{
+    uint32_t e = k0;
+    bool more = false;
+    uint32_t nxt = 0;
+    if (live) {
+        const uint32_t w = k1 - k0;   // candidates k0 .. k0 + w
+        uint32_t v = b.q[0].y;        // start k0 <= ip always
+#pragma unroll
+        for (int t = 1; t < 8; t++) {
+            const u32x4a &c = b.q[t >> 1];
+            const uint32_t st = (t & 1) ? c.z : c.x, va = (t & 1) ? c.w : c.y;
+            if (w >= (uint32_t)t && ip >= st) v = va;
+        }
+        e = v;
+        more = w > 7u && ip >= b.q[3].z;
+        nxt = k0 + 8u;
+    }
+    while (__ballot(more)) {
+        u32x4a c{0u, 0u, 0u, 0u};
+        if (more) c = *(const u32x4a *)(pairs + 2 * (size_t)nxt);
+        if (more) {
+            if (ip >= c.x) e = c.y;
+            if (nxt + 1u <= k1 && ip >= c.z) e = c.w;
+            more = nxt + 1u < k1 && ip >= c.z;
+            nxt += 2u;
+        }
+    }
+    return e;
+}
+
 // Pass 2: rte_lpm_lookup's tbl8 step for valid+extended entries, then the
 // verdicts of stage FW (firewall.c:183-210) and stage LPM. Packets that did
 // not reach the coprocessor (stage P drop) keep their verdict. Counts the
 // FW stage's pkt_total / pkt_not_ipv4 (firewall.h:56-61) over valid packets.
-// LPM_T8 false: the route's tbl8 step was done by the caller (tbl8_issue /
-// tbl8_finish).
+// LPM_T8 false: the route's second round was done by the caller (tbl8_issue /
+// tbl8_finish, or bkt_pairs_issue / bkt_pairs_finish).
 template <int FW, int LPM, int PPT, bool LPM_T8 = true>
 __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[PPT], const uint32_t (&src)[PPT],
                                       const uint32_t (&dst)[PPT], const bool (&valid)[PPT], uint32_t (&fwe)[PPT],
@@ -798,7 +851,7 @@ __device__ __forceinline__ void pass2(const CopKParams &p, const uint32_t (&w3)[
     if (FW == COPK_TBL_BKT) bkt_step<PPT>(p.fw_bpairs, src, fwe, fwe2, reached);
     if (LPM == COPK_TBL_DIR && LPM_T8) tbl8_step<PPT>(p.lpm_tbl8, p.lpm_tbl8_packed, dst, lpe);
     if (LPM == COPK_TBL_TRIE) trie_walk<PPT>(p.lpm_tnodes, p.lpm_tleaves, dst, lpe, reached);
-    if (LPM == COPK_TBL_BKT) bkt_step<PPT>(p.lpm_bpairs, dst, lpe, lpe2, reached);
+    if (LPM == COPK_TBL_BKT && LPM_T8) bkt_step<PPT>(p.lpm_bpairs, dst, lpe, lpe2, reached);
 #pragma unroll
     for (int k = 0; k < PPT; k++) {
         if (!reached[k]) continue;

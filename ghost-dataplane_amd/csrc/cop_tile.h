@@ -196,18 +196,26 @@ __device__ __forceinline__ void hit_sort_out(const CopKParams &p, const HitLds &
 #ifndef COPK_IMIX_STEPS
 #define COPK_IMIX_STEPS 1
 #endif
+// The bucketed route form (COP_CFG_LPM_BKT) on the step path too: its
+// index and pair rounds pipelined across steps like DIR-24-8's tbl24 and
+// tbl8 probes (1), or the whole-tile body (0)
+#ifndef COPK_BKT_STEPS
+#define COPK_BKT_STEPS 1
+#endif
 
 // Whether a tile can run step by step (tile_steps): segmented lists, no
 // optional feature, the firewall in LDS, and coalesced 64-byte slots with
 // the route in LDS or DIR-24-8 (whose two dependent probes tile_steps_v
 // pipelines across steps; the trie's and the bucketed form's chains are
-// not), or IMIX with a DIR-24-8 route.
+// not; the bucketed form's two rounds are, COPK_BKT_STEPS), or IMIX with a
+// DIR-24-8 or bucketed route.
 template <int FW, int LPM, int LAY, bool EXT>
 constexpr bool steps_ok()
 {
     return !EXT && FW != COPK_TBL_DIR && FW != COPK_TBL_BKT &&
-           ((LAY == COPK_LAY_COALESCED && LPM != COPK_TBL_TRIE && LPM != COPK_TBL_BKT) ||
-            (LAY == COPK_LAY_IMIX && COPK_IMIX_STEPS && LPM == COPK_TBL_DIR));
+           ((LAY == COPK_LAY_COALESCED && LPM != COPK_TBL_TRIE && (LPM != COPK_TBL_BKT || COPK_BKT_STEPS)) ||
+            (LAY == COPK_LAY_IMIX && COPK_IMIX_STEPS &&
+             (LPM == COPK_TBL_DIR || (LPM == COPK_TBL_BKT && COPK_BKT_STEPS))));
 }
 
 // One tile of the poll-mode kernel, step by step (tile_body does the same
@@ -480,11 +488,13 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
         // offsets. (The whole-tile body instead waits for every step's
         // offsets, then every step's headers, then the probes: four
         // dependent round trips with nothing else in flight.)
-        static_assert(LPM == COPK_TBL_DIR && FW != COPK_TBL_DIR && FW != COPK_TBL_BKT, "IMIX steps: DIR-24-8 route");
+        static_assert((LPM == COPK_TBL_DIR || LPM == COPK_TBL_BKT) && FW != COPK_TBL_DIR && FW != COPK_TBL_BKT,
+                      "IMIX steps: DIR-24-8 or bucketed route");
         struct St {
-            uint32_t w3, src, dst, verdict, port, fwe, lpe;
+            uint32_t w3, src, dst, verdict, port, fwe, lpe, lpe2;
             bool valid;
             T8 t8;
+            BkQ bq;
         };
         St a{}, b{}, c{};
         u32x4 h[3];
@@ -499,26 +509,32 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
                 gather_step(sg, h, w3[0], w6[0], w7[0], w8[0]);
                 uint32_t verdict[1], port[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1];
                 pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2, fwe2);
-                a = St{w3[0], src[0], dst[0], verdict[0], port[0], fwe[0], lpe[0],
-                       base + step_off<PPT>(k, wave) + (uint32_t)lane < B.n && B.n != 0, T8{false, 0ull}};
+                a = St{w3[0], src[0], dst[0], verdict[0], port[0], fwe[0], lpe[0], lpe2[0],
+                       base + step_off<PPT>(k, wave) + (uint32_t)lane < B.n && B.n != 0, T8{false, 0ull}, BkQ{}};
                 if (k + 1 < PPT) {
                     load_step_imix(sg, B.pkts, off, B.data_off, h, sys);
                     if (k + 2 < PPT) off = load_off_imix(B.offsets, base + step_off<PPT>(k + 2, wave), lane, last, sys);
                 }
             }
-            if (k >= 1 && k <= PPT) b.t8 = tbl8_issue(p.lpm_tbl8, p.lpm_tbl8_packed, b.dst, b.lpe);
+            if (k >= 1 && k <= PPT) {
+                if constexpr (LPM == COPK_TBL_BKT) b.bq = bkt_pairs_issue(p.lpm_bpairs, b.lpe, b.verdict == COPK_FORWARD);
+                else b.t8 = tbl8_issue(p.lpm_tbl8, p.lpm_tbl8_packed, b.dst, b.lpe);
+            }
             if (k >= 2) {
                 const uint32_t w3[1] = {c.w3}, src[1] = {c.src}, dst[1] = {c.dst}, lpe2[1] = {0}, fwe2[1] = {0};
                 const bool valid[1] = {c.valid};
                 uint32_t verdict[1] = {c.verdict}, fwe[1] = {c.fwe}, flags[1], rnh[1], ct = 0, cn = 0;
-                uint32_t lpe[1] = {tbl8_finish(p.lpm_tbl8, p.lpm_tbl8_packed, c.dst, c.lpe, c.t8)};
+                uint32_t lpe[1];
+                if constexpr (LPM == COPK_TBL_BKT)
+                    lpe[0] = bkt_pairs_finish(p.lpm_bpairs, c.dst, c.lpe, c.lpe2, c.verdict == COPK_FORWARD, c.bq);
+                else lpe[0] = tbl8_finish(p.lpm_tbl8, p.lpm_tbl8_packed, c.dst, c.lpe, c.t8);
                 pass2<FW, LPM, 1, false>(p, w3, src, dst, valid, fwe, lpe, lpe2, fwe2, verdict, flags, rnh, ct, cn);
                 emit(k - 2, valid[0], verdict[0], flags[0], c.port, rnh[0]);
             }
             c = b;
             b = a;
         }
-    } else if constexpr (LPM != COPK_TBL_DIR) {
+    } else if constexpr (LPM != COPK_TBL_DIR && LPM != COPK_TBL_BKT) {
         // LDS-only lookups: each step classified as its headers land
 #pragma unroll
         for (int k = 0; k < PPT; k++) {
@@ -543,16 +559,19 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
         }
     } else {
         // The route's DIR-24-8 probes: two dependent global loads per packet
-        // (tbl24, then tbl8 for an extended entry: most wave-steps have one).
+        // (tbl24, then tbl8 for an extended entry: most wave-steps have one);
+        // or the bucketed form's two L2 rounds (the bucket index, then eight
+        // pairs), the same pipeline.
         // A three-step pipeline keeps them off the step's critical path: in
         // round k, step k's headers are gathered and classified and its tbl24
         // probe issued, step k - 1's tbl8 load is issued (its tbl24 entry has
         // landed), and step k - 2 is finished and written out.
         static_assert(FW != COPK_TBL_DIR && FW != COPK_TBL_BKT, "firewall lookups in LDS only");
         struct St {
-            uint32_t w3, src, dst, verdict, port, fwe, lpe;
+            uint32_t w3, src, dst, verdict, port, fwe, lpe, lpe2;
             bool valid;
             T8 t8;
+            BkQ bq;
         };
         St a{}, b{}, c{};
 #pragma unroll
@@ -566,15 +585,21 @@ __device__ __forceinline__ void tile_steps_v(const CopKParams &p, const LdsCarve
                               sys);
                 uint32_t verdict[1], port[1], fwe[1], lpe[1], lpe2[1], fwe2[1], src[1], dst[1];
                 pass1<FW, LPM, 1>(p, tb, w3, w6, w7, w8, verdict, port, src, dst, fwe, lpe, lpe2, fwe2);
-                a = St{w3[0], src[0], dst[0], verdict[0], port[0], fwe[0], lpe[0],
-                       base + step_off<PPT>(k, wave) + (uint32_t)lane < B.n && B.n != 0, T8{false, 0ull}};
+                a = St{w3[0], src[0], dst[0], verdict[0], port[0], fwe[0], lpe[0], lpe2[0],
+                       base + step_off<PPT>(k, wave) + (uint32_t)lane < B.n && B.n != 0, T8{false, 0ull}, BkQ{}};
             }
-            if (k >= 1 && k <= PPT) b.t8 = tbl8_issue(p.lpm_tbl8, p.lpm_tbl8_packed, b.dst, b.lpe);
+            if (k >= 1 && k <= PPT) {
+                if constexpr (LPM == COPK_TBL_BKT) b.bq = bkt_pairs_issue(p.lpm_bpairs, b.lpe, b.verdict == COPK_FORWARD);
+                else b.t8 = tbl8_issue(p.lpm_tbl8, p.lpm_tbl8_packed, b.dst, b.lpe);
+            }
             if (k >= 2) {
                 const uint32_t w3[1] = {c.w3}, src[1] = {c.src}, dst[1] = {c.dst}, lpe2[1] = {0}, fwe2[1] = {0};
                 const bool valid[1] = {c.valid};
                 uint32_t verdict[1] = {c.verdict}, fwe[1] = {c.fwe}, flags[1], rnh[1], ct = 0, cn = 0;
-                uint32_t lpe[1] = {tbl8_finish(p.lpm_tbl8, p.lpm_tbl8_packed, c.dst, c.lpe, c.t8)};
+                uint32_t lpe[1];
+                if constexpr (LPM == COPK_TBL_BKT)
+                    lpe[0] = bkt_pairs_finish(p.lpm_bpairs, c.dst, c.lpe, c.lpe2, c.verdict == COPK_FORWARD, c.bq);
+                else lpe[0] = tbl8_finish(p.lpm_tbl8, p.lpm_tbl8_packed, c.dst, c.lpe, c.t8);
                 pass2<FW, LPM, 1, false>(p, w3, src, dst, valid, fwe, lpe, lpe2, fwe2, verdict, flags, rnh, ct, cn);
                 emit(k - 2, valid[0], verdict[0], flags[0], c.port, rnh[0]);
             }

@@ -233,3 +233,74 @@ def test_fw_bkt_beside_small_or_trie_routes(gpu_ctx_factory, route):
         m.run(2)
     res = dr.download(cg.RESULT_DT, n)
     assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
+
+
+@pytest.mark.parametrize("layout", ["slots", "imix"])
+def test_bkt_route_on_the_step_path(gpu_ctx_factory, layout):
+    """The bucketed route form (CFG_LPM_BKT) on the poll-mode step path
+    (segmented lists: its index and pair rounds pipelined across steps,
+    bkt_pairs_issue / bkt_pairs_finish, with the wide-bucket rounds inside
+    the finish): 100 host routes in one /24 among 30k random routes, a
+    quarter of the destinations steered into that /24 and its neighbours;
+    64-byte slots and IMIX; records, segment lists and counters against the
+    oracle over posts that wrap the ring."""
+    from test_gpu_seg import nseg, seg_to_dense
+    fw_rules = cg.gen_rules(0x5EED1081, 1000, cg.GEN_FW, 20)
+    dense = np.zeros(100, dtype=cg.PREFIX_DT)
+    dense["ip"] = 0x0A0B0C00 + 2 * np.arange(100, dtype=np.uint32)
+    dense["depth"] = 32
+    dense["next_hop"] = 100 + np.arange(100)
+    routes = np.concatenate([cg.gen_rules(0x5EED2096, 30000, cg.GEN_ROUTES, 0), dense])
+    rtt = cg.LpmTable(routes, 1 << 20, 1 << 16, False)
+    ctx = gpu_ctx_factory(stages=S | F | L, flags=cg.CFG_LPM_BKT | cg.CFG_SEG_LISTS)
+    ctx.set_fw_table(cg.LpmTable(fw_rules, 1024, 24, True))
+    ctx.set_route_lpm(rtt)
+    assert ctx.route_form() == "bkt"
+    ofw = orc.OracleLpm(1024, 24)
+    ofw.setup(fw_rules["ip"], fw_rules["depth"], fw_rules["next_hop"])
+    ort = orc.OracleLpm(1 << 20, 1 << 16)
+    ort.setup(routes["ip"], routes["depth"], routes["next_hop"], stop_at_error=False)
+    B, P = 65536, 3
+    rng = np.random.default_rng(9)
+    ips = np.arange(0x0A0B0B00, 0x0A0B0E00, dtype=np.uint32)
+    if layout == "imix":
+        slab, offs = cg.gen_imix(0x5EED0083, B, fw_rules, routes)
+        sel = rng.choice(B, B // 4, replace=False)
+        for i, d in zip(sel, ips[rng.integers(0, len(ips), len(sel))]):
+            slab[offs[i] + 30:offs[i] + 34] = np.array([d], dtype=">u4").view(np.uint8)
+        per = slab.nbytes + offs.nbytes
+        dp = ctx.alloc(per * P)
+        for s_ in range(P):
+            dp.upload(slab, s_ * per)
+            dp.upload(offs, s_ * per + slab.nbytes)
+        ro, fo, co = orc.process(slab, B, offsets=offs, stages=S | F | L, fw=ofw, route=ort)
+        kname, ros, fos = "cop_pmd<1, 4, 1, 4, false>", [ro] * P, [fo] * P
+    else:
+        pk = cg.gen_trace(0x5EED0083, B * P, fw_rules, routes)
+        pk2 = pk.reshape(B * P, 64)
+        sel = rng.choice(B * P, B * P // 4, replace=False)
+        pk2[sel, 30:34] = ips[rng.integers(0, len(ips), len(sel))].astype(">u4").view(np.uint8).reshape(-1, 4)
+        per = B * 64
+        dp = ctx.alloc(per * P)
+        dp.upload(pk)
+        outs = [orc.process(pk[s_ * per:(s_ + 1) * per], B, stages=S | F | L, fw=ofw, route=ort) for s_ in range(P)]
+        kname, ros, fos = "cop_pmd<1, 4, 2, 4, false>", [o[0] for o in outs], [o[1] for o in outs]
+    assert ((ros[0]["flags"] & 1) == 1).mean() > 0.3
+    dr = ctx.alloc(B * P * 8)
+    df = ctx.alloc(B * P * 4)
+    dc = ctx.alloc(P * nseg(B) * 4)
+    if layout == "imix":
+        ring = cg.make_ring(dp, P, B, dr, per, offsets=dp.addr + slab.nbytes, offsets_slot_words=per // 4,
+                            fwd_idx=df, fwd_count=dc)
+    else:
+        ring = cg.make_ring(dp, P, B, dr, per, stride=64, fwd_idx=df, fwd_count=dc)
+    with ctx.pmd_start(ring) as m:
+        assert m.info()["kernel_name"] == kname, m.info()
+        m.run(7)
+    res = dr.download(cg.RESULT_DT, B * P)
+    fwd = df.download(np.uint32, B * P)
+    cnt = dc.download(np.uint32, P * nseg(B))
+    for s_ in range(P):
+        assert np.array_equal(res[s_ * B:(s_ + 1) * B].view(np.uint8), ros[s_].view(np.uint8)), f"slot {s_}"
+        got = seg_to_dense(fwd[s_ * B:(s_ + 1) * B], cnt[s_ * nseg(B):(s_ + 1) * nseg(B)], B)
+        assert np.array_equal(got, fos[s_]), f"slot {s_} list"
