@@ -135,6 +135,7 @@ SIGNATURES = {
     "cop_pmd_wait": (c_int, [c_void_p, c_uint64]),
     "cop_pmd_posted": (c_uint64, [c_void_p]),
     "cop_pmd_run": (c_int, [c_void_p, c_uint64]),
+    "cop_pmd_run_timed": (c_int, [c_void_p, c_uint64, POINTER(c_uint64), POINTER(c_uint64)]),
     "cop_pmd_info": (c_int, [c_void_p, POINTER(PmdInfo)]),
     "cop_pmd_stop": (c_int, [c_void_p]),
     "cop_pmd_start_rings": (c_int, [c_void_p, POINTER(BatchRing), c_uint32, c_uint32, POINTER(c_void_p)]),
@@ -702,6 +703,9 @@ class Pmd:
         # a measurable part of a 30 us post)
         L = lib()
         self._post, self._wait, self._run = L.cop_pmd_post, L.cop_pmd_wait, L.cop_pmd_run
+        self._run_timed = L.cop_pmd_run_timed
+        self._t = (c_uint64(0), c_uint64(0))
+        self._tp = (byref(self._t[0]), byref(self._t[1]))
         self._n_posted = 0   # every post goes through this object
 
     def post(self, count: int):
@@ -719,6 +723,16 @@ class Pmd:
         if rc < 0:
             _check(rc, self.ctx, "pmd_run")
         self._n_posted += count
+
+    def run_timed(self, count: int):
+        """run(count), returning (t_post_ns, t_done_ns): CLOCK_MONOTONIC taken
+        inside the library just before the first post and just after the
+        last completion (cop_pmd_run_timed)."""
+        rc = self._run_timed(self.handle, count, *self._tp)
+        if rc < 0:
+            _check(rc, self.ctx, "pmd_run_timed")
+        self._n_posted += count
+        return self._t[0].value, self._t[1].value
 
     @property
     def posted(self) -> int:

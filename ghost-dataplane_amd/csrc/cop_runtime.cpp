@@ -15,6 +15,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -2804,6 +2805,24 @@ int cop_pmd_run(cop_pmd *m, uint64_t count)
         done += k;
     }
     return cop_pmd_wait(m, m->ring[0].posted.load());
+}
+
+static uint64_t mono_ns()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+int cop_pmd_run_timed(cop_pmd *m, uint64_t count, uint64_t *t_post_ns, uint64_t *t_done_ns)
+{
+    if (!m) return -EINVAL;
+    const uint64_t t0 = mono_ns();
+    const int rc = cop_pmd_run(m, count);
+    const uint64_t t1 = mono_ns();
+    if (t_post_ns) *t_post_ns = t0;
+    if (t_done_ns) *t_done_ns = t1;
+    return rc;
 }
 
 int cop_pmd_info(const cop_pmd *m, cop_pmd_info_t *out)

@@ -423,6 +423,10 @@ uint64_t cop_pmd_posted(const cop_pmd *pmd);
 /* Post `count` batches (in posts of a quarter ring, so it never drains) and
  * wait for all of them: one synchronous burst. 0 or -errno. */
 int cop_pmd_run(cop_pmd *pmd, uint64_t count);
+/* cop_pmd_run, stamped: CLOCK_MONOTONIC (ns) just before the first post and
+ * just after the last batch is seen complete (benchmarks: the window of the
+ * library call itself, no caller overhead in it). 0 or -errno. */
+int cop_pmd_run_timed(cop_pmd *pmd, uint64_t count, uint64_t *t_post_ns, uint64_t *t_done_ns);
 typedef struct cop_pmd_info_t {
     uint32_t workers;          /* worker workgroups (all co-resident) */
     uint32_t workers_per_cu;
