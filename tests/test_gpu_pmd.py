@@ -415,3 +415,47 @@ def test_pmd_imix_steps_ragged_and_rewritten(gpu_ctx_factory, flags):
             assert np.array_equal(res.view(np.uint8), ro.view(np.uint8)), f"generation {g} records"
             assert np.array_equal(seg_to_dense(fwd, cnt, B), fo), f"generation {g} list"
         assert m.info()["launches"] == 1
+
+
+@pytest.mark.parametrize("stages", [S | F | L, F | L, S | L, L])
+@pytest.mark.parametrize("form", ["dir", "bkt"])
+def test_pmd_imix_steps_stage_masks(gpu_ctx_factory, stages, form):
+    """The IMIX step path (segmented lists) with every stage mask that keeps
+    the route stage, and both route forms it pipelines (DIR-24-8's tbl24 /
+    tbl8, the bucketed index / pairs): the stage-P drop, the firewall's
+    verdict and the route's next hop of every packet, and the segment lists,
+    against the oracle."""
+    from test_gpu_seg import nseg, seg_to_dense
+    rules = fw1k()
+    rts = routes(30000)
+    ctx = gpu_ctx_factory(stages=stages, flags=cg.CFG_SEG_LISTS | (cg.CFG_LPM_BKT if form == "bkt" else 0))
+    ctx.set_fw_table(cg.LpmTable(rules, 1024, 24, True))
+    ctx.set_route_lpm(cg.LpmTable(rts, 1 << 20, 1 << 16, False))
+    assert ctx.route_form() == form
+    B, P = 30001, 2
+    opts = cg.trace_opts(pct_bad_version=5, pct_non_ipv4=5, pct_unknown_dst=5)
+    slab, offs = cg.gen_imix(0x5EED0B70 + stages, B, rules, rts, opts=opts)
+    per = ((slab.nbytes + offs.nbytes + 4095) // 4096) * 4096
+    dp = ctx.alloc(per * P)
+    for s_ in range(P):
+        dp.upload(slab, s_ * per)
+        dp.upload(offs, s_ * per + slab.nbytes)
+    FS = ((B + 3) // 4) * 4
+    dr = ctx.alloc(B * P * 8)
+    df = ctx.alloc(FS * P * 4)
+    dc = ctx.alloc(P * nseg(B) * 4)
+    ring = cg.make_ring(dp, P, B, dr, per, offsets=dp.addr + slab.nbytes, offsets_slot_words=per // 4,
+                        fwd_idx=df, fwd_slot=FS, fwd_count=dc)
+    with ctx.pmd_start(ring) as m:
+        fw_part = 1 if stages & F else 0
+        lpm_part = 4 if form == "bkt" else 2
+        assert m.info()["kernel_name"] == f"cop_pmd<{fw_part}, {lpm_part}, 1, 4, false>", m.info()
+        m.run(5)
+    fw, rt = oracle_tables(rules, rts)
+    ro, fo, _ = orc.process(slab, B, offsets=offs, stages=stages, fw=fw, route=rt)
+    res = dr.download(cg.RESULT_DT, B * P)
+    fwd = df.download(np.uint32, FS * P)
+    cnt = dc.download(np.uint32, P * nseg(B))
+    for s_ in range(P):
+        assert np.array_equal(res[s_ * B:(s_ + 1) * B].view(np.uint8), ro.view(np.uint8)), f"slot {s_}"
+        assert np.array_equal(seg_to_dense(fwd[s_ * FS:s_ * FS + B], cnt[s_ * nseg(B):(s_ + 1) * nseg(B)], B), fo)
