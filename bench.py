@@ -705,9 +705,10 @@ def e2e_leg(args, dev) -> dict:
     """North star: packets start and end in host memory. The end-to-end rate
     of cop_process_host_stream over an mbuf-like host pool (NB_MBUF = 131072
     buffers 2176 bytes apart, data at 128 bytes of headroom, init.h:38-44),
-    visited `passes` times: the host threads gather each batch's 16-byte header
-    records into pinned staging (and copy the previous batch's 8-byte records
-    out), hipMemcpyAsync H2D, the pipeline (stage P + firewall, fw1k), D2H;
+    visited `passes` times: the host threads gather each batch's 12-byte header
+    records (COP_HDR12_STRIDE) into pinned staging (and copy the previous
+    batch's 8-byte records out), hipMemcpyAsync H2D, the pipeline (stage P +
+    firewall, fw1k), the records written into mapped pinned memory;
     lanes (HIP streams, not threads) overlap batches. Host threads = the
     job's CPU share, the caller included (HIP's own runtime threads aside):
     the count the CPU baseline's multicore leg runs. Checked against the device-resident
@@ -758,7 +759,8 @@ def e2e_leg(args, dev) -> dict:
             row = {"lanes": lanes, "host_threads": thr, "batch": batch,
                    "zero_copy": {0: "none", 1: "staging + records", 2: "records"}[zc],
                    "mpkt_s": round(n / t / 1e6, 3),
-                   "h2d_gb_s": round(n * 16 / t / 1e9, 2), "d2h_gb_s": round(n * 8 / t / 1e9, 2),
+                   "header_record_bytes": 12, "h2d_gb_s": round(n * 12 / t / 1e9, 2),
+                   "d2h_gb_s": round(n * 8 / t / 1e9, 2),
                    "runs_ms": [round(x * 1e3, 3) for x in times], "matches_device_records": ok}
             res["rows"].append(row)
             log(f"[rank 0] e2e {row}")

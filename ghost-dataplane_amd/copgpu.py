@@ -32,6 +32,7 @@ MAX_DEMUX_PORTS = 8
 GEN_FW, GEN_ROUTES = 0, 1
 UNKNOWN_PORT = 0xFFFF
 HDR16_STRIDE = 16   # packed header records: frame bytes 12..15 + 24..35 per packet
+HDR12_STRIDE = 12   # compact records (one-shot batches): frame bytes 12..15 + 26..33 per packet
 
 PREFIX_DT = np.dtype([("ip", "<u4"), ("next_hop", "<u4"), ("depth", "u1"), ("_pad", "u1", (3,))])
 RESULT_DT = np.dtype([("verdict", "u1"), ("flags", "u1"), ("port", "<u2"), ("route_nh", "<u4")])
@@ -149,6 +150,7 @@ SIGNATURES = {
     "cop_process_host_stream": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p]),
     "cop_set_host_threads": (c_int, [c_void_p, c_uint32]),
     "cop_pack_headers": (None, [c_void_p, c_uint32, c_void_p]),
+    "cop_pack_headers12": (None, [c_void_p, c_uint32, c_void_p]),
     "cop_counters_read": (c_int, [c_void_p, c_void_p, c_int]),
     "cop_counters_device_ptr": (c_void_p, [c_void_p]),
     "cop_rule_counters_read": (c_int, [c_void_p, c_void_p, c_uint32, c_int]),
@@ -258,6 +260,14 @@ def pack_headers_np(frames: np.ndarray, n: int, stride: int = 64) -> np.ndarray:
     """The same records from a contiguous frame array, in numpy (tests)."""
     f = np.asarray(frames, np.uint8)[: n * stride].reshape(n, stride)
     return np.ascontiguousarray(np.concatenate([f[:, 12:16], f[:, 24:36]], axis=1)).reshape(-1)
+
+
+def pack_headers12(ptrs: np.ndarray) -> np.ndarray:
+    """cop_pack_headers12 over host packet addresses (u64 array): n x 12 bytes."""
+    ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+    out = np.zeros(len(ptrs) * HDR12_STRIDE, np.uint8)
+    lib().cop_pack_headers12(ptrs.ctypes.data, len(ptrs), out.ctypes.data)
+    return out
 
 
 def prefixes(ip, depth, next_hop) -> np.ndarray:

@@ -117,13 +117,24 @@ struct GatherPool {
     size_t cp_bytes = 0;
     int parts = 1;
 
-    // packed header records (COP_HDR16_STRIDE): frame bytes 12..15, 24..35
-    static void slice(const void *const *src, uint8_t *dst, uint32_t n, int parts, int i)
+    // packed header records: 16 bytes (COP_HDR16_STRIDE: frame bytes 12..15,
+    // 24..35) or 12 (COP_HDR12_STRIDE: 12..15, 26..33)
+    static void slice(const void *const *src, uint8_t *dst, uint32_t n, int parts, int i, uint32_t rec = 16)
     {
         const uint32_t lo = (uint32_t)((uint64_t)n * i / parts), hi = (uint32_t)((uint64_t)n * (i + 1) / parts);
         // scattered mbuf reads are DRAM-latency bound: keep PF lines in flight
         constexpr uint32_t PF = 16;
         for (uint32_t q = lo; q < hi && q < lo + PF; q++) __builtin_prefetch((const uint8_t *)src[q] + 12);
+        if (rec == COP_HDR12_STRIDE) {
+            for (uint32_t q = lo; q < hi; q++) {
+                if (q + PF < hi) __builtin_prefetch((const uint8_t *)src[q + PF] + 12);
+                const uint8_t *p = (const uint8_t *)src[q];
+                uint8_t *d = dst + (size_t)q * COP_HDR12_STRIDE;
+                memcpy(d, p + 12, 4);
+                memcpy(d + 4, p + 26, 8);
+            }
+            return;
+        }
         for (uint32_t q = lo; q < hi; q++) {
             if (q + PF < hi) __builtin_prefetch((const uint8_t *)src[q + PF] + 12);
             const uint8_t *p = (const uint8_t *)src[q];
@@ -132,16 +143,23 @@ struct GatherPool {
             memcpy(d + 4, p + 24, 12);
         }
     }
-    // slice i of the job: the copy-out slice (64-byte aligned pieces), then the gather slice
+    uint32_t rec = 16;   // the job's record size
+    // the job's slices: jparts of them, participant i takes slice i - joff
+    // (a synchronous job: the caller is participant 0 and takes slice 0; an
+    // asynchronous one: the workers alone)
+    int jparts = 1, joff = 0;
+    // participant i's slice of the job: the copy-out slice (64-byte aligned
+    // pieces), then the gather slice
     void part(int i)
     {
+        i -= joff;
         if (cp_bytes) {
             const size_t units = (cp_bytes + 63) / 64;
-            const size_t lo = std::min(cp_bytes, units * (size_t)i / parts * 64),
-                         hi = std::min(cp_bytes, units * (size_t)(i + 1) / parts * 64);
+            const size_t lo = std::min(cp_bytes, units * (size_t)i / jparts * 64),
+                         hi = std::min(cp_bytes, units * (size_t)(i + 1) / jparts * 64);
             if (hi > lo) memcpy(cp_dst + lo, cp_src + lo, hi - lo);
         }
-        if (n) slice(src, dst, n, parts, i);
+        if (n) slice(src, dst, n, jparts, i, rec);
     }
     void worker(int i)
     {
@@ -174,27 +192,45 @@ struct GatherPool {
     // one job on every participant: gather n packets' records into d_, and
     // copy cp_n bytes from cp_s to cp_d (either may be empty)
     void run(const void *const *s_, uint8_t *d_, uint32_t n_, const void *cp_s = nullptr, void *cp_d = nullptr,
-             size_t cp_n = 0)
+             size_t cp_n = 0, uint32_t rec_ = 16)
     {
         if (th.empty() || (n_ < 4096 && cp_n < (size_t)1 << 18)) {
             if (cp_n) memcpy(cp_d, cp_s, cp_n);
-            if (n_) slice(s_, d_, n_, 1, 0);
+            if (n_) slice(s_, d_, n_, 1, 0, rec_);
             return;
         }
+        rec = rec_;
+        post(s_, d_, n_, cp_s, cp_d, cp_n, false);
+        part(0);
+        wait();
+    }
+    // the same job on the workers alone; the caller goes on (wait() joins it)
+    void start_async(const void *const *s_, uint8_t *d_, uint32_t n_, const void *cp_s = nullptr,
+                     void *cp_d = nullptr, size_t cp_n = 0, uint32_t rec_ = 16)
+    {
+        rec = rec_;
+        post(s_, d_, n_, cp_s, cp_d, cp_n, true);
+    }
+    void wait()
+    {
+        while (pending.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+    }
+    void post(const void *const *s_, uint8_t *d_, uint32_t n_, const void *cp_s, void *cp_d, size_t cp_n, bool async)
+    {
         src = s_;
         dst = d_;
         n = n_;
         cp_src = (const uint8_t *)cp_s;
         cp_dst = (uint8_t *)cp_d;
         cp_bytes = cp_n;
+        jparts = async ? (int)th.size() : parts;
+        joff = async ? 1 : 0;
         pending.store((int)th.size(), std::memory_order_relaxed);
         gen.fetch_add(1, std::memory_order_seq_cst);
         if (sleepers.load(std::memory_order_seq_cst)) {
             std::lock_guard<std::mutex> lk(m);   // (a sleeper checks gen under the lock)
             cv.notify_all();
         }
-        part(0);
-        while (pending.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
     }
     void gather(const void *const *s_, uint8_t *d_, uint32_t n_) { run(s_, d_, n_); }
     ~GatherPool()
@@ -272,6 +308,10 @@ struct cop_ctx {
     // instead of 24), staging and records both mapped and moved by the
     // kernel over PCIe (1), or both copied (0); $COP_STREAM_ZC
     int stream_zc = 2;
+    // cop_process_host_stream's staged header record: COP_HDR12_STRIDE
+    // (default: src and dst only, a quarter fewer bytes over PCIe) or
+    // COP_HDR16_STRIDE; $COP_STREAM_REC
+    uint32_t stream_rec = COP_HDR12_STRIDE;
     uint8_t *zc_stage = nullptr;      // mapped pinned: records in
     cop_result *zc_res = nullptr;     // mapped pinned: results out
     uint32_t *zc_fwd = nullptr;       // mapped pinned: forward list + count
@@ -564,6 +604,7 @@ int cop_create(const cop_config *cfg_in, cop_ctx **out)
     if (const char *e = getenv("COP_LDS_PAD")) c->lds_pad = (uint32_t)strtoul(e, nullptr, 0) & ~15u;
     if (const char *e = getenv("COP_ZC_MAX")) c->zc_max = (uint32_t)strtoul(e, nullptr, 0);
     if (const char *e = getenv("COP_STREAM_ZC")) c->stream_zc = std::min(2, std::max(0, atoi(e)));
+    if (const char *e = getenv("COP_STREAM_REC")) c->stream_rec = atoi(e) == 16 ? COP_HDR16_STRIDE : COP_HDR12_STRIDE;
     if (const char *e = getenv("COP_LOADS")) c->coalesced = strcmp(e, "strided") != 0;
     if (const char *e = getenv("COP_STAGE_LISTS")) c->stage_lists = atoi(e) != 0;
     if (const char *e = getenv("COP_HIT_BINS")) c->hit_bins = atoi(e) != 0;
@@ -947,7 +988,7 @@ struct Plan {
 static Plan plan_launch(const cop_ctx *c, uint64_t total, bool imix, uint32_t min_stride)
 {
     const bool wide = !imix && min_stride >= COPK_COALESCED_MIN_STRIDE;
-    const bool hdr16 = !imix && min_stride == COP_HDR16_STRIDE;
+    const bool hdr16 = !imix && (min_stride == COP_HDR16_STRIDE || min_stride == COP_HDR12_STRIDE);
     return Plan{choose_ppt(c, total, imix),
                 imix    ? COPK_LAY_IMIX
                 : hdr16 ? COPK_LAY_HDR16
@@ -1190,11 +1231,14 @@ static int submit_on(cop_ctx *c, Lane &L, const cop_batch *batches, uint32_t nb,
             return set_err(c, -EINVAL, "batches in one submit must all be slot or all IMIX");
         if (b.n > c->cfg.max_batch) return set_err(c, -EINVAL, "batch %u: n %u > max_batch", i, b.n);
         if (b.n && (!b.pkts || !b.results)) return set_err(c, -EINVAL, "batch %u: null pointer", i);
-        if (((uintptr_t)b.pkts & 15) || (b.data_off & 15) || (!imix && (b.stride & 15)) ||
-            (!imix && b.stride < 36 && b.stride != COP_HDR16_STRIDE))
+        // (12-byte records are read as dwords: 4-byte aligned starts suffice)
+        const bool rec12 = !imix && b.stride == COP_HDR12_STRIDE;
+        if (((uintptr_t)b.pkts & (rec12 ? 3 : 15)) || (b.data_off & 15) || (!imix && !rec12 && (b.stride & 15)) ||
+            (!imix && !rec12 && b.stride < 36 && b.stride != COP_HDR16_STRIDE))
             return set_err(c, -EINVAL, "batch %u: packet starts must be 16-byte aligned", i);
-        if (!imix && b.n && (b.stride == COP_HDR16_STRIDE) != (batches[0].stride == COP_HDR16_STRIDE))
-            return set_err(c, -EINVAL, "batches in one submit must all be header records or all frames");
+        if (!imix && b.n && b.stride != batches[0].stride &&
+            (b.stride <= COP_HDR16_STRIDE || batches[0].stride <= COP_HDR16_STRIDE))
+            return set_err(c, -EINVAL, "batches in one submit must all be 16-byte records, 12-byte records or frames");
         if ((uintptr_t)b.results & 7) return set_err(c, -EINVAL, "batch %u: results misaligned", i);
         total += b.n;
         if (b.fwd_idx || b.fwd_count) compact = true;
@@ -1324,6 +1368,11 @@ int cop_poll(cop_ctx *c)
 void cop_pack_headers(const void *const *pkt_data, uint32_t n, uint8_t *out)
 {
     GatherPool::slice(pkt_data, out, n, 1, 0);
+}
+
+void cop_pack_headers12(const void *const *pkt_data, uint32_t n, uint8_t *out)
+{
+    GatherPool::slice(pkt_data, out, n, 1, 0, COP_HDR12_STRIDE);
 }
 
 static void host_gather(cop_ctx *c, const void *const *src, uint8_t *dst, uint32_t n)
@@ -1567,9 +1616,11 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
     if (!c || (n && (!pkt_data || !results)) || batch == 0) return -EINVAL;
     if (batch > c->cfg.max_batch) return set_err(c, -EINVAL, "batch %u > max_batch", batch);
     if (int rc = sync_lanes(c)) return rc;
-    // zc 1: staging and records mapped; 2: records mapped, staging copied
+    // zc 1: staging and records mapped; 2: records mapped, staging copied.
+    // rec: the staged header record, 12 bytes (default) or 16
     const int zc = c->stream_zc;
     const bool zc_in = zc == 1, zc_out = zc != 0;
+    const uint32_t rec = c->stream_rec;
     for (int l = 0; l < c->n_lanes; l++) {
         Lane &L = c->lane[l];
         if (L.cap >= batch && L.zc == zc) continue;
@@ -1601,37 +1652,53 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
         }
         L.cap = batch;
     }
-    int lane = 0;
-    for (uint64_t first = 0; first < n; first += batch) {
-        Lane &L = c->lane[lane];
-        lane = (lane + 1) % c->n_lanes;
-        const uint32_t k = (uint32_t)((n - first) < batch ? (n - first) : batch);
-        // the lane's previous batch: wait for it, then one job on the host
-        // threads copies its records out and gathers this batch's 16-byte
-        // header records (the other lanes' batches are in flight meanwhile)
+    // Batch bi runs on lane bi % n_lanes. Preparing it waits for that lane's
+    // previous batch, copies that batch's records out and gathers bi's
+    // header records into the lane's staging. With two or more lanes and a
+    // gather pool, batch bi + 1 is prepared by the pool's workers while the
+    // caller issues batch bi's copy and launch (whose API calls would
+    // otherwise sit between two gathers); one lane reuses one staging, so it
+    // prepares in line.
+    const uint64_t nb = (n + batch - 1) / batch;
+    const bool overlap = c->gather && c->gather->th.size() > 0 && c->n_lanes > 1;
+    auto prepare = [&](uint64_t bi, bool async) -> int {
+        Lane &L = c->lane[bi % (uint64_t)c->n_lanes];
+        const uint64_t first = bi * batch;
+        const uint32_t k = (uint32_t)std::min<uint64_t>(batch, n - first);
         const cop_result *prev = nullptr;
         uint32_t prev_n = 0;
+        uint64_t prev_first = 0;
         if (L.busy) {
             HIPCHK(c, hipEventSynchronize(L.done));
             L.busy = false;
             prev = L.h_res;
             prev_n = L.n;
+            prev_first = L.first;
         }
-        if (c->gather) {
-            c->gather->run(pkt_data + first, L.h_stage, k, prev, prev ? results + L.first : nullptr,
-                           (size_t)prev_n * sizeof(cop_result));
+        cop_result *prev_dst = prev ? results + prev_first : nullptr;
+        const size_t prev_bytes = (size_t)prev_n * sizeof(cop_result);
+        if (c->gather && async) {
+            c->gather->start_async(pkt_data + first, L.h_stage, k, prev, prev_dst, prev_bytes, rec);
+        } else if (c->gather) {
+            c->gather->run(pkt_data + first, L.h_stage, k, prev, prev_dst, prev_bytes, rec);
         } else {
-            if (prev_n) memcpy(results + L.first, prev, (size_t)prev_n * sizeof(cop_result));
-            host_gather(c, pkt_data + first, L.h_stage, k);
+            if (prev_n) memcpy(prev_dst, prev, prev_bytes);
+            GatherPool::slice(pkt_data + first, L.h_stage, k, 1, 0, rec);
         }
+        return 0;
+    };
+    auto issue = [&](uint64_t bi) -> int {
+        Lane &L = c->lane[bi % (uint64_t)c->n_lanes];
+        const uint64_t first = bi * batch;
+        const uint32_t k = (uint32_t)std::min<uint64_t>(batch, n - first);
         // (c->dbg & 0x100: timing ablation, the H2D copy skipped; results wrong)
         if (!zc_in && !(c->dbg & 0x100u))
-            HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * COP_HDR16_STRIDE, hipMemcpyHostToDevice, L.s));
+            HIPCHK(c, hipMemcpyAsync(L.d_stage, L.h_stage, (size_t)k * rec, hipMemcpyHostToDevice, L.s));
         cop_batch b;
         memset(&b, 0, sizeof(b));
         b.pkts = zc_in ? L.m_stage : L.d_stage;
         b.n = k;
-        b.stride = COP_HDR16_STRIDE;
+        b.stride = rec;
         b.results = zc_out ? L.m_res : L.d_res;
         if (int rc = submit_on(c, L, &b, 1, false, c->cfg.stages)) return rc;
         if (!zc_out) HIPCHK(c, hipMemcpyAsync(L.h_res, L.d_res, (size_t)k * 8, hipMemcpyDeviceToHost, L.s));
@@ -1639,6 +1706,19 @@ int cop_process_host_stream(cop_ctx *c, const void *const *pkt_data, uint64_t n,
         L.busy = true;
         L.first = first;
         L.n = k;
+        return 0;
+    };
+    if (nb)
+        if (int rc = prepare(0, false)) return rc;
+    for (uint64_t bi = 0; bi < nb; bi++) {
+        const bool pre = overlap && bi + 1 < nb;
+        if (pre)
+            if (int rc = prepare(bi + 1, true)) return rc;
+        const int rc = issue(bi);
+        if (pre) c->gather->wait();   // (also on an error: the workers are done with the staging)
+        if (rc) return rc;
+        if (!overlap && bi + 1 < nb)
+            if (int rc2 = prepare(bi + 1, false)) return rc2;
     }
     for (int l = 0; l < c->n_lanes; l++)
         if (int rc = lane_finish(c, c->lane[l], results)) return rc;

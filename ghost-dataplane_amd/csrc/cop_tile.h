@@ -687,6 +687,21 @@ __device__ __forceinline__ bool tile_body(const CopKParams &p, const Opt &o, con
         for (int k = 0; k < PPT; k++) load_step_imix(sg, B.pkts, off[k], B.data_off, v[k], sys);
 #pragma unroll
         for (int k = 0; k < PPT; k++) gather_step(sg, v[k], w3[k], w6[k], w7[k], w8[k]);
+    } else if (LAY == COPK_LAY_HDR16 && B.n && B.stride == 12u) {
+        // one 12-byte record per packet (COP_HDR12_STRIDE, one-shot batches):
+        // frame bytes 12..15, then 26..29 (src) and 30..33 (dst); bytes
+        // 24..35 rebuilt around them as pass1 reads them (the rest unread)
+#pragma unroll
+        for (int k = 0; k < PPT; k++) {
+            const uint32_t ic = min(base + k * BLOCK + tid, last);
+            const uint32_t *r = (const uint32_t *)(B.pkts + B.data_off + (size_t)ic * 12u);
+            const uint32_t a = __builtin_nontemporal_load(r), s_ = __builtin_nontemporal_load(r + 1),
+                           d_ = __builtin_nontemporal_load(r + 2);
+            w3[k] = a;
+            w6[k] = s_ << 16;
+            w7[k] = (s_ >> 16) | (d_ << 16);
+            w8[k] = d_ >> 16;
+        }
     } else if (LAY == COPK_LAY_HDR16 && B.n) {
         // one 16-byte record per packet: frame bytes 12..15 then 24..35
 #pragma unroll

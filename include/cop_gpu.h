@@ -290,6 +290,14 @@ int  cop_load_fw_rules_file(cop_ctx *ctx, const char *path, const cop_lpm_config
  * this way instead of a 64-byte header line. */
 #define COP_HDR16_STRIDE 16u
 void cop_pack_headers(const void *const *pkt_data, uint32_t n, uint8_t *out /* n * 16 bytes */);
+/* Compact header records (cop_submit batches only, not rings): stride ==
+ * COP_HDR12_STRIDE holds one 12-byte record per packet (pkts 4-byte
+ * aligned), frame bytes 12..15 then 26..33 (src, dst): the bytes the
+ * verdicts depend on, a quarter fewer
+ * than a 16-byte record. Results are identical to the frames'. The
+ * end-to-end host path (cop_process_host_stream) sends these. */
+#define COP_HDR12_STRIDE 12u
+void cop_pack_headers12(const void *const *pkt_data, uint32_t n, uint8_t *out /* n * 12 bytes */);
 
 /* One batch of packets resident in device memory (HBM).
  * Packet i starts at  pkts + (offsets ? offsets[i] : i * stride) + data_off.

@@ -278,16 +278,19 @@ def test_process_host_stream_lanes(gpu_ctx_factory, lanes, threads):
     assert np.array_equal(res.view(np.uint8), ro.view(np.uint8))
 
 
-@pytest.mark.parametrize("lanes,threads,zc", [(2, 16, 0), (4, 5, 0), (2, 16, 1), (3, 1, 1), (4, 16, 2), (1, 3, 2)])
-def test_process_host_stream_large_batches(gpu_ctx_factory, monkeypatch, lanes, threads, zc):
+@pytest.mark.parametrize("lanes,threads,zc,rec", [(2, 16, 0, 16), (4, 5, 0, 12), (2, 16, 1, 12), (3, 1, 1, 16),
+                                                   (4, 16, 2, 12), (1, 3, 2, 12), (4, 16, 2, 16), (2, 1, 2, 12)])
+def test_process_host_stream_large_batches(gpu_ctx_factory, monkeypatch, lanes, threads, zc, rec):
     """The end-to-end path as bench.py's e2e leg runs it: 256k-packet
     batches, the records of each lane's previous batch copied out by the host
     threads in the same job as the next gather (GatherPool::run), a ragged
     last batch; 3 x 262144 + 77 packets, each of a 50k-packet mbuf pool
     visited many times, against the oracle. zc: staging and records in
     mapped pinned memory, read and written by the kernel over PCIe
-    ($COP_STREAM_ZC, no copy-engine transfers)."""
+    ($COP_STREAM_ZC 1), records only (2, the default) or neither (0); rec:
+    12-byte (the default) or 16-byte header records ($COP_STREAM_REC)."""
     monkeypatch.setenv("COP_STREAM_ZC", str(zc))
+    monkeypatch.setenv("COP_STREAM_REC", str(rec))
     rules = fw1k()
     ctx = setup_ctx(gpu_ctx_factory, rules, n_streams=lanes, max_batch=262144)
     ctx.set_host_threads(threads)
@@ -470,4 +473,27 @@ def test_every_tile_width_same_records(gpu_ctx_factory, monkeypatch, ppt):
     fwo, rto = oracle_tables(rules, routes)
     ro, fo, _ = orc.process(pk, n, stages=S | F | L, fw=fwo, route=rto)
     rg, fg, _ = gpu_run(ctx, pk, n, batches=3)
+    assert_parity(rg, fg, ro, fo)
+
+
+@pytest.mark.parametrize("stages", [S | F, F, S | F | L])
+def test_hdr12_records_match_frames(gpu_ctx_factory, stages):
+    """12-byte header records (COP_HDR12_STRIDE: frame bytes 12..15 then
+    26..33, what cop_process_host_stream sends by default) give the frames'
+    exact records and forward lists: odd batch sizes in one submit, packets
+    with bad versions, non-IPv4 EtherTypes and unknown destinations, the
+    route stage on."""
+    rules = fw1k()
+    routes = routes100k(n=20000)
+    ctx = setup_ctx(gpu_ctx_factory, rules, routes, stages=stages)
+    n = 70001
+    opts = cg.trace_opts(pct_bad_version=7, pct_non_ipv4=7, pct_unknown_dst=7)
+    pk = cg.gen_trace(0x5EED0903, n, rules, routes, opts=opts)
+    base = pk.ctypes.data
+    rec = cg.pack_headers12((base + np.arange(n, dtype=np.uint64) * 64).astype(np.uint64))
+    f = pk.reshape(n, 64)
+    assert np.array_equal(rec.reshape(n, 12), np.concatenate([f[:, 12:16], f[:, 26:34]], axis=1))
+    fwo, rto = oracle_tables(rules, routes)
+    ro, fo, _ = orc.process(pk, n, stages=stages, fw=fwo, route=rto)
+    rg, fg, _ = gpu_run(ctx, rec, n, stride=cg.HDR12_STRIDE, batches=3)
     assert_parity(rg, fg, ro, fo)

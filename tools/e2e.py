@@ -3,7 +3,8 @@
 end in host memory ... pinned hipMemcpyAsync in and out"): packets sit in an
 mbuf-like host pool (NB_MBUF = 131072 buffers at 2176 B stride, data at
 128 B headroom, init.h:38-44); cop_process_host_stream packs each batch's
-16-byte header records (COP_HDR16_STRIDE: frame bytes 12..15, 24..35) into
+12-byte header records (COP_HDR12_STRIDE: frame bytes 12..15, 26..33; or 16,
+$COP_STREAM_REC) into
 pinned staging, copies H2D, runs the pipeline,
 copies the 8-byte records D2H, with the lanes overlapping (or, zc, the
 kernel reads and writes mapped pinned memory: $COP_STREAM_ZC); the gather
@@ -62,7 +63,7 @@ def main():
                     ctx.process_host_stream(ptrs, batch, out=out)
                     ts.append(time.perf_counter() - t0)
                 dt = float(np.median(ts))
-                print(f"{lanes:5d} {threads:3d} {zc:2d} {batch:7d} {n / dt / 1e6:9.1f} {n * cg.HDR16_STRIDE / dt / 1e9:9.2f}  "
+                print(f"{lanes:5d} {threads:3d} {zc:2d} {batch:7d} {n / dt / 1e6:9.1f} {n * int(os.environ.get("COP_STREAM_REC", "12")) / dt / 1e9:9.2f}  "
                       f"{'ok' if ok else 'MISMATCH'}", flush=True)
                 ctx.close()
     # batch size at the default mode (larger copies, fewer per-batch calls)
@@ -80,9 +81,27 @@ def main():
             ctx.process_host_stream(ptrs, batch, out=out)
             ts.append(time.perf_counter() - t0)
         dt = float(np.median(ts))
-        print(f"{lanes:5d} {threads:3d}  2 {batch:7d} {n / dt / 1e6:9.1f} {n * cg.HDR16_STRIDE / dt / 1e9:9.2f}  "
+        print(f"{lanes:5d} {threads:3d}  2 {batch:7d} {n / dt / 1e6:9.1f} {n * int(os.environ.get("COP_STREAM_REC", "12")) / dt / 1e9:9.2f}  "
               f"{'ok' if ok else 'MISMATCH'}", flush=True)
         ctx.close()
+    # 16-byte records against the default 12-byte ones ($COP_STREAM_REC)
+    for rec in (16, 12, 16, 12):
+        os.environ["COP_STREAM_REC"] = str(rec)
+        ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=4, max_batch=131072)
+        ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
+        ctx.set_host_threads(share)
+        res = ctx.process_host_stream(ptrs[:NB_MBUF], 131072)
+        ok = np.array_equal(res.view(np.uint8), ro.view(np.uint8))
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            ctx.process_host_stream(ptrs, 131072, out=out)
+            ts.append(time.perf_counter() - t0)
+        dt = float(np.median(ts))
+        print(f"records {rec:2d} B, 4 lanes, {share} threads, 131072: {n / dt / 1e6:.1f} Mpkt/s, "
+              f"{n * rec / dt / 1e9:.2f} GB/s H2D  {'ok' if ok else 'MISMATCH'}", flush=True)
+        ctx.close()
+    os.environ.pop("COP_STREAM_REC", None)
     # timing ablations at the default mode: no H2D copy ($COP_DBG 0x100;
     # results wrong), and no gather (the same 131072 records every batch)
     for what, env in (("no H2D copy", {"COP_DBG": "0x100"}),):
