@@ -44,14 +44,17 @@ def main():
     # host threads never above the job's CPU share ($OMP_NUM_THREADS, 16 on
     # the pool's one-GPU boxes): more gather threads than cores collapse
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    rec_b = int(os.environ.get("COP_STREAM_REC", "12"))
+    lanes_l = [int(x) for x in os.environ.get("E2E_LANES", "2,4").split(",")]
+    thr_l = [int(x) for x in os.environ.get("E2E_THREADS", "1,2,4,8,12,16").split(",")]
     print(f"{'lanes':>5s} {'thr':>3s} {'zc':>2s} {'batch':>7s} {'Mpkt/s':>9s} {'GB/s H2D':>9s}  parity", flush=True)
     for zc in (int(x) for x in os.environ.get("E2E_MODES", "0,1,2").split(",")):
         os.environ["COP_STREAM_ZC"] = str(zc)
-        for lanes in (2, 4):
-            for threads in (1, 2, 4, 8, 12, 16):
+        for lanes in lanes_l:
+            for threads in thr_l:
                 if threads > share:
                     continue
-                batch = 262144
+                batch = int(os.environ.get("E2E_BATCH", "262144"))
                 ctx = cg.Context(stages=cg.STAGE_PARSE | cg.STAGE_FW, n_streams=lanes, max_batch=batch)
                 ctx.set_fw_table(cg.LpmTable(fw, 1024, 24))
                 ctx.set_host_threads(threads)
@@ -63,7 +66,7 @@ def main():
                     ctx.process_host_stream(ptrs, batch, out=out)
                     ts.append(time.perf_counter() - t0)
                 dt = float(np.median(ts))
-                print(f"{lanes:5d} {threads:3d} {zc:2d} {batch:7d} {n / dt / 1e6:9.1f} {n * int(os.environ.get("COP_STREAM_REC", "12")) / dt / 1e9:9.2f}  "
+                print(f"{lanes:5d} {threads:3d} {zc:2d} {batch:7d} {n / dt / 1e6:9.1f} {n * rec_b / dt / 1e9:9.2f}  "
                       f"{'ok' if ok else 'MISMATCH'}", flush=True)
                 ctx.close()
     # batch size at the default mode (larger copies, fewer per-batch calls)
@@ -81,7 +84,7 @@ def main():
             ctx.process_host_stream(ptrs, batch, out=out)
             ts.append(time.perf_counter() - t0)
         dt = float(np.median(ts))
-        print(f"{lanes:5d} {threads:3d}  2 {batch:7d} {n / dt / 1e6:9.1f} {n * int(os.environ.get("COP_STREAM_REC", "12")) / dt / 1e9:9.2f}  "
+        print(f"{lanes:5d} {threads:3d}  2 {batch:7d} {n / dt / 1e6:9.1f} {n * rec_b / dt / 1e9:9.2f}  "
               f"{'ok' if ok else 'MISMATCH'}", flush=True)
         ctx.close()
     # 16-byte records against the default 12-byte ones ($COP_STREAM_REC)
