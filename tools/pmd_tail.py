@@ -101,8 +101,11 @@ def main():
             if not len(v):
                 continue
             share = slow[:, sel].sum() / max(1, slow.sum())
+            sv, bv = np.array(seens)[:, sel], np.array(bodies)[:, sel]
             print(f"  {name} {g:2d}: workers {sel.sum():4d}  median {np.median(v):5.1f}  p90 {np.percentile(v, 90):5.1f}"
-                  f"  max {v.max():5.1f}  share of the slowest 5 % {share:5.3f}")
+                  f"  max {v.max():5.1f}  share of the slowest 5 % {share:5.3f}"
+                  f"  (seen {np.nanmedian(sv):4.2f}, body {np.nanmedian(bv):5.2f}, counted after body "
+                  f"{np.nanmedian(v - (sv + bv)[~np.isnan(E[:, sel])]):4.2f})")
 
     split("XCD (w % 8)", w % 8, 8)
     split("slot on CU (w // 256)", w // 256, 5)
