@@ -115,42 +115,13 @@ __device__ __forceinline__ void pmd_leave(const CopKPmd &P, uint32_t why)
 // slot spent on a doorbell. Leaders also turn the host's stop flag, a
 // look-back timeout or an idle spell (no new post on any ring for
 // idle_ticks) into the exit word.
-// XCD-local relays (COPK_PMD_XRELAY, one ring): each XCD has a doorbell
-// leader of its own (the first of its workers to claim it at the census;
-// the XCD from the XCC_ID hardware register), which raises ITS XCD's relay
-// line with a plain store: the line stays in that XCD's L2, and the XCD's
-// workers poll it with non-temporal loads (L1 bypassed, served by the L2),
-// an L2 round trip instead of the memory-side one of an agent-scope poll of
-// a line another XCD's atomic wrote. Nothing crosses XCDs but the gate
-// (published before any relay, as before), which non-leaders also read every
-// 16th poll with the exit word: a fallback that never leaves a worker
-// waiting for a relay that did not come.
-// COPK_PMD_XRELAY=2, a fan-out instead: the leaders and relays stay as
-// they are, and the first worker of an XCD whose agent-scope poll sees a new
-// relay value raises an XCD-local line (a workgroup-scope atomic max, done
-// in that XCD's L2), which the XCD's other workers poll with non-temporal
-// loads; each worker's own agent-scope poll runs every fourth poll.
-#ifndef COPK_PMD_XRELAY
-#define COPK_PMD_XRELAY 0
-#endif
-__device__ __forceinline__ __attribute__((unused)) uint32_t xcc_id()
-{
-    // s_getreg_b32 HW_REG_XCC_ID (hwreg 20), bits [3:0]
-    return __builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & 7u;
-}
-
 __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd &P, uint32_t r, uint32_t wr,
-                                                                  unsigned long long b, bool leader, int xcc = -1)
+                                                                  unsigned long long b, bool leader)
 {
     // this worker's copy of the relay (one 128-byte line per group of the
     // ring's workers): a thousand pollers on one line would hammer one
     // memory channel while other workers stream
-    const bool xr = xcc >= 0 && COPK_PMD_XRELAY == 1;   // XCD-local relays: line xcc, raised by this XCD's leader only
-    const bool xf = xcc >= 0 && COPK_PMD_XRELAY == 2;   // fan-out: XCD-local copies of the relays (one ring)
-    unsigned long long *relay =
-        P.d_posted + ((size_t)r * COPK_PMD_RELAYS + (xr ? (uint32_t)xcc : wr % COPK_PMD_RELAYS)) * 16;
-    // (fan-out: ring 1's relay lines, unused with one ring)
-    unsigned long long *xline = xf ? P.d_posted + ((size_t)COPK_PMD_RELAYS + (uint32_t)xcc) * 16 : nullptr;
+    unsigned long long *relay = P.d_posted + ((size_t)r * COPK_PMD_RELAYS + wr % COPK_PMD_RELAYS) * 16;
     unsigned long long *relays = P.d_posted + (size_t)r * COPK_PMD_RELAYS * 16;
     unsigned long long *gate = P.d_gate + (size_t)r * 16;
     const unsigned long long *h_posted = P.h_posted + (size_t)r * 8;
@@ -158,11 +129,8 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
     for (uint32_t spins = 0;; spins++) {
         // every load of a poll is issued before any is used: one round trip
         // per poll, not one per load (a leader's PCIe read overlaps the rest)
-        const bool far = xf ? (leader || (spins & 3u) == 3u) : (!xr || leader || (spins & 15u) == 15u);
-        const unsigned long long hl = xf ? __builtin_nontemporal_load(xline) : 0ull;
-        const unsigned long long hp = xr ? __builtin_nontemporal_load(relay) : (!xf || far) ? ld_u64(relay) : 0ull;
-        const uint32_t ex = far ? ld_agent(&P.d_ctl[0]) : 0u;
-        const unsigned long long gx = (xr && far) ? ld_u64(gate) : 0ull;
+        const unsigned long long hp = ld_u64(relay);
+        const uint32_t ex = ld_agent(&P.d_ctl[0]);
         unsigned long long h = 0;
         uint32_t stop = 0;
         if (leader) {
@@ -170,13 +138,7 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
             h = __hip_atomic_load(h_posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             stop = __hip_atomic_load(P.h_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        if (xf && hl > b) return hl;
-        if (hp > b) {
-            if (xf) __hip_atomic_fetch_max(xline, hp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return hp;
-        }
-        // (XCD-local relays: the gate's published count, the fallback)
-        if (xr && !(gx >> COPK_PMD_GATE_SHIFT) && (gx & GATE_POSTED) > b) return gx & GATE_POSTED;
+        if (hp > b) return hp;
         if (ex) {
             if (ex == COPK_PMD_ABORT) return 0;
             // idle or stop: the gate was closed before the exit word was set
@@ -189,10 +151,7 @@ __device__ __attribute__((unused)) unsigned long long wait_posted(const CopKPmd 
         if (leader) {
             const unsigned long long now = __builtin_amdgcn_s_memrealtime();
             if (h > hp && (COPK_PMD_NOGATE || gate_publish(gate, h, hp))) {
-                if (xr) __builtin_nontemporal_store(h, relay);   // this XCD's line, kept in its L2
-                else
-                    for (int x = 0; x < COPK_PMD_RELAYS; x++) atomicMax(relays + x * 16, h);
-                if (xf) __hip_atomic_fetch_max(xline, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int x = 0; x < COPK_PMD_RELAYS; x++) atomicMax(relays + x * 16, h);
                 if (P.stamps && r == 0) {   // diagnostic: when each doorbell value was relayed
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2], h);
                     st_stamp(&P.stamps[(size_t)P.n_work * 8 + (h % 64) * 2 + 1], now);
@@ -274,18 +233,8 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
     uint32_t *s_door = lc.s_misc + 36;   // [0..1] posted, [2] leave, [3] the batch's packets
     stage_tables<FW, LPM>(p, lc.tb, lane, wave);
 
-    // census: every worker and the doorbell resident, or nobody works. With
-    // XCD-local relays (one ring) the first worker of each XCD to claim its
-    // XCD's word in the gate line (words 8..15, zeroed per launch) is that
-    // XCD's doorbell leader
-    int xcc = -1;
-    bool xlead = false;
+    // census: every worker and the doorbell resident, or nobody works
     if (tid == 0) {
-        if (COPK_PMD_XRELAY && P.n_rings == 1) {
-            xcc = (int)xcc_id();
-            if (COPK_PMD_XRELAY == 1)
-                xlead = atomicCAS((unsigned long long *)&P.d_gate[8 + xcc], 0ull, 1ull) == 0ull;
-        }
         atomicAdd(&P.d_ctl[1], 1u);
         uint32_t spins = 0;
         while (ld_agent(&P.d_ctl[1]) < P.n_work && ld_agent(&P.d_ctl[0]) == 0) {
@@ -324,7 +273,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
         uint32_t slot = (uint32_t)(b % n_slots);
         const uint32_t qb = G / tpb, rb = G % tpb;
         unsigned long long posted = 0;
-        const bool leader = (xcc >= 0 && COPK_PMD_XRELAY == 1) ? xlead : wr % P.relay_stride == 0;
+        const bool leader = wr % P.relay_stride == 0;
         unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
         // the tile's completion, by one lane once every wave's stores
         // (write-through) and counter adds have landed: count it for its
@@ -358,7 +307,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             if (b >= posted) {
                 // wait for batch b to be posted (one lane polls the relay)
                 if (tid == 0) {
-                    const unsigned long long hp = wait_posted(P, r, wr, b, leader, xcc);
+                    const unsigned long long hp = wait_posted(P, r, wr, b, leader);
                     s_door[0] = (uint32_t)hp;
                     s_door[1] = (uint32_t)(hp >> 32);
                     s_door[2] = hp == 0 ? 1u : 0u;
@@ -496,7 +445,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
             unsigned long long *ticket = P.d_ticket + ((size_t)r * COPK_PMD_TK_LANES + xl) * 16;
             uint32_t *s_tk = lc.s_misc + 72;   // the next claimed ticket (lo, hi)
             unsigned long long *stamp = P.stamps ? P.stamps + (size_t)blockIdx.x * 8 : nullptr;
-            const bool leader = (xcc >= 0 && COPK_PMD_XRELAY == 1) ? xlead : wr % P.relay_stride == 0;
+            const bool leader = wr % P.relay_stride == 0;
             unsigned long long posted = 0;
             // lane 0 of wave 0: the pending slot count (issued after a tile's
             // stores drained, its return read one tile later)
@@ -555,7 +504,7 @@ __global__ __launch_bounds__(BLOCK, COPK_PMD_WAVES_PER_EU(PPT)) void cop_pmd(con
                         // count first (it may complete a batch), then wait
                         if (tid == 0) {
                             pend_flush();
-                            const unsigned long long hp = wait_posted(P, r, wr, b, leader, xcc);
+                            const unsigned long long hp = wait_posted(P, r, wr, b, leader);
                             s_door[0] = (uint32_t)hp;
                             s_door[1] = (uint32_t)(hp >> 32);
                             s_door[2] = hp == 0 ? 1u : 0u;
